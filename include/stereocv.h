@@ -1,0 +1,128 @@
+/*
+ * stereocv.h -- C ABI of libstereocv.so, the MI355X (gfx950) stereo cost-volume and
+ * disparity-regression engine.
+ *
+ * Every entry point replaces one operator of babiking/realtime_stereo_matcher's hot
+ * path (file:line cited per function).  Conventions shared by all entry points:
+ *
+ *   - Pointers are DEVICE pointers (HIP).  The library never allocates, frees or
+ *     synchronises caller memory; all work is enqueued on `stream` (a hipStream_t
+ *     passed as void*, NULL = the null stream) and is stream-ordered.  No host sync,
+ *     no global mutable state except the thread-local error string.
+ *   - Feature maps are 4-D (N, C, H, W).  `l_strides` / `r_strides` give the element
+ *     strides of (N, C, H, W); the W stride must be 1 (the caller makes rows
+ *     contiguous).  NULL strides mean contiguous.
+ *   - Outputs are dense, contiguous, in the layout stated per function.
+ *   - dtype codes: SM_F32, SM_F16, SM_BF16 (the output dtype equals the input dtype
+ *     unless the function says otherwise).  Accumulation is always fp32 or wider.
+ *   - Return 0 on success, a negative SM_E* code on failure; sm_last_error() then
+ *     returns a thread-local, human-readable message.
+ */
+#ifndef STEREOCV_H_
+#define STEREOCV_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum sm_dtype { SM_F32 = 0, SM_F16 = 1, SM_BF16 = 2 };
+enum sm_status { SM_OK = 0, SM_EINVAL = -1, SM_EDTYPE = -2, SM_ELAUNCH = -3 };
+enum sm_argext_mode { SM_ARGMIN = 0, SM_ARGMAX = 1 };
+enum sm_regress_flags {
+  SM_REGRESS_SOFTMAX = 0,      /* softmax over D inside (mobile_disp_net_c.py:208-220) */
+  SM_REGRESS_PRESOFTMAXED = 1  /* input already softmaxed (mobile_stereo_net_v4.py:10-14) */
+};
+/* Inner-product kernel selection (sm_cv_inner_product_ex). */
+enum sm_ip_algo {
+  SM_IP_AUTO = 0,     /* library default for the shape/dtype */
+  SM_IP_VALU = 1,     /* fp32 VALU, LDS-staged right window reused across the D sweep */
+  SM_IP_MFMA_F32 = 2  /* banded C-contraction on v_mfma_f32_16x16x4_f32 (exact fp32 fma chain) */
+};
+
+/* Library version (major*10000 + minor*100 + patch). */
+int sm_version(void);
+/* Thread-local message for the last failing call on this thread ("" if none). */
+const char* sm_last_error(void);
+
+/* a-1: TorchInnerProductCost(max_disparity)(left, right)
+ *      -- cost_volume/inner_product.py:11-42
+ * out[n,d,y,x] = sum_c L[n,c,y,x] * R[n,c,y,x-d] (x >= d), 0 (x < d).
+ * out: (N, D, H, W), dtype = dtype. */
+int sm_cv_inner_product(const void* left, const void* right, void* out, int dtype,
+                        int64_t N, int64_t C, int64_t H, int64_t W, int64_t D,
+                        const int64_t* l_strides, const int64_t* r_strides, void* stream);
+/* Same with an explicit kernel choice (enum sm_ip_algo). */
+int sm_cv_inner_product_ex(const void* left, const void* right, void* out, int dtype,
+                           int64_t N, int64_t C, int64_t H, int64_t W, int64_t D,
+                           const int64_t* l_strides, const int64_t* r_strides, int algo,
+                           void* stream);
+
+/* a-6: make_correlation_volume(l_fmap, r_fmap, max_disp)
+ *      -- model/mobile_disp_net_c.py:188-205
+ * out[n,d,y,x] = mean_c L*R(x-d) (x >= d), 0 (x < d).  out: (N, D, H, W). */
+int sm_cv_correlation_mean(const void* left, const void* right, void* out, int dtype,
+                           int64_t N, int64_t C, int64_t H, int64_t W, int64_t D,
+                           const int64_t* l_strides, const int64_t* r_strides, void* stream);
+
+/* a-2: TorchGroupwiseCost(n_groups, max_disparity)(left, right)
+ *      -- cost_volume/groupwise.py:24-56
+ * out[n,g,y,x,d] = mean_{c in group g} L*R(x-d) (x >= d), 0 (x < d);
+ * groups are contiguous channel blocks of C/G.  out: (N, G, H, W, D) float32 always
+ * (groupwise.py:39).  C % G != 0 -> SM_EINVAL. */
+int sm_cv_groupwise(const void* left, const void* right, float* out, int dtype,
+                    int64_t N, int64_t C, int64_t H, int64_t W, int64_t D, int64_t G,
+                    const int64_t* l_strides, const int64_t* r_strides, void* stream);
+
+/* a-3: TorchConcatenateCost(max_disparity)(left, right)
+ *      -- cost_volume/concatenate.py:11-41
+ * out[n,c,y,x,d] = L (x >= d) ; out[n,C+c,y,x,d] = R(x-d) (x >= d) ; 0 (x < d).
+ * out: (N, 2C, H, W, D), bit-exact copy. */
+int sm_cv_concat(const void* left, const void* right, void* out, int dtype,
+                 int64_t N, int64_t C, int64_t H, int64_t W, int64_t D,
+                 const int64_t* l_strides, const int64_t* r_strides, void* stream);
+
+/* a-4: TorchInterweaveCost()(left, right) -- cost_volume/interweave.py:10-22,
+ *      = interweave_tensors -- model/mobile_stereo_net_v4.py:17-23
+ * out[n,2c] = L[n,c], out[n,2c+1] = R[n,c].  out: (N, 2C, H, W), bit-exact. */
+int sm_cv_interweave(const void* left, const void* right, void* out, int dtype,
+                     int64_t N, int64_t C, int64_t H, int64_t W,
+                     const int64_t* l_strides, const int64_t* r_strides, void* stream);
+
+/* a-4': the v4 per-disparity shifted interweave materialised as one volume
+ *      -- model/mobile_stereo_net_v4.py:443-461 (input of the Conv3d stack)
+ * out[n,2c,d,y,x] = L[n,c,y,x], out[n,2c+1,d,y,x] = R[n,c,y,x-d] (x >= d), 0 (x < d).
+ * out: (N, 2C, D, H, W), bit-exact. */
+int sm_cv_interweave_shifted(const void* left, const void* right, void* out, int dtype,
+                             int64_t N, int64_t C, int64_t H, int64_t W, int64_t D,
+                             const int64_t* l_strides, const int64_t* r_strides, void* stream);
+
+/* a-5: make_cost_volume(left, right, max_disp) -- model/mobile_stereo_net.py:8-27
+ * out[n,c,d,y,x] = L[n,c,y,x] - R[n,c,y,x-d] (x >= d), 1.0 (x < d).
+ * out: (N, C, D, H, W), bit-exact (one subtraction in the input dtype). */
+int sm_cv_diff(const void* left, const void* right, void* out, int dtype,
+               int64_t N, int64_t C, int64_t H, int64_t W, int64_t D,
+               const int64_t* l_strides, const int64_t* r_strides, void* stream);
+
+/* a-7: soft-argmin regression over D of a (N, D, H, W) volume
+ *   flags = SM_REGRESS_SOFTMAX:      sum_d d * softmax_d(v)   (mobile_disp_net_c.py:208-220,
+ *                                    inline mobile_stereo_net.py:144-147)
+ *   flags = SM_REGRESS_PRESOFTMAXED: sum_d d * v              (mobile_stereo_net_v4.py:10-14)
+ * out: (N, H, W) in `dtype` (keepdim is a caller-side view).  fp64 accumulation.
+ * vol_strides: element strides of (N, D, H, W), W stride must be 1 (NULL = contiguous). */
+int sm_regress_softargmin(const void* volume, void* out, int dtype,
+                          int64_t N, int64_t D, int64_t H, int64_t W, int flags,
+                          const int64_t* vol_strides, void* stream);
+
+/* a-8: hard argmin / argmax over D (build-defined): first index on ties,
+ * NaN counts as the extreme (torch.argmin/argmax semantics).  out: (N, H, W) int64. */
+int sm_regress_argext(const void* volume, int64_t* out, int dtype,
+                      int64_t N, int64_t D, int64_t H, int64_t W, int mode,
+                      const int64_t* vol_strides, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* STEREOCV_H_ */

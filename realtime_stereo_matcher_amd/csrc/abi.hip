@@ -1,0 +1,118 @@
+// extern "C" entry points of libstereocv.so (declared in include/stereocv.h).
+#include "common.h"
+
+namespace smcv {
+int dot_volume_valu_entry(const void* left, const void* right, void* out, int dtype, int64_t N,
+                          int64_t C, int64_t H, int64_t W, int64_t D, int64_t G,
+                          const int64_t* l_strides, const int64_t* r_strides, int mode,
+                          void* stream);
+int ip_mfma_entry(const void* left, const void* right, void* out, int dtype, int64_t N,
+                  int64_t C, int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
+                  const int64_t* r_strides, void* stream, bool* handled);
+int concat_entry(const void* left, const void* right, void* out, int dtype, int64_t N,
+                 int64_t C, int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
+                 const int64_t* r_strides, void* stream);
+int interweave_entry(const void* left, const void* right, void* out, int dtype, int64_t N,
+                     int64_t C, int64_t H, int64_t W, const int64_t* l_strides,
+                     const int64_t* r_strides, void* stream);
+int shifted_entry(const void* left, const void* right, void* out, int dtype, int64_t N,
+                  int64_t C, int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
+                  const int64_t* r_strides, int mode, void* stream);
+int softargmin_entry(const void* volume, void* out, int dtype, int64_t N, int64_t D, int64_t H,
+                     int64_t W, int flags, const int64_t* vol_strides, void* stream);
+int argext_entry(const void* volume, int64_t* out, int dtype, int64_t N, int64_t D, int64_t H,
+                 int64_t W, int mode, const int64_t* vol_strides, void* stream);
+}  // namespace smcv
+
+using namespace smcv;
+
+#define SM_ENTRY_BEGIN last_error().clear();
+
+extern "C" int sm_cv_inner_product_ex(const void* left, const void* right, void* out, int dtype,
+                                      int64_t N, int64_t C, int64_t H, int64_t W, int64_t D,
+                                      const int64_t* l_strides, const int64_t* r_strides,
+                                      int algo, void* stream) {
+  SM_ENTRY_BEGIN
+  if (algo != SM_IP_AUTO && algo != SM_IP_VALU && algo != SM_IP_MFMA_F32)
+    return fail(SM_EINVAL, "unknown inner-product algo");
+  if (algo == SM_IP_AUTO || algo == SM_IP_MFMA_F32) {
+    bool handled = false;
+    int rc = ip_mfma_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, stream,
+                           &handled);
+    if (handled || rc != SM_OK) return rc;
+    if (algo == SM_IP_MFMA_F32)
+      return fail(SM_EINVAL, "MFMA inner product does not support this shape/dtype");
+  }
+  return dot_volume_valu_entry(left, right, out, dtype, N, C, H, W, D, 1, l_strides, r_strides,
+                               0, stream);
+}
+
+extern "C" int sm_cv_inner_product(const void* left, const void* right, void* out, int dtype,
+                                   int64_t N, int64_t C, int64_t H, int64_t W, int64_t D,
+                                   const int64_t* l_strides, const int64_t* r_strides,
+                                   void* stream) {
+  return sm_cv_inner_product_ex(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides,
+                                SM_IP_AUTO, stream);
+}
+
+extern "C" int sm_cv_correlation_mean(const void* left, const void* right, void* out, int dtype,
+                                      int64_t N, int64_t C, int64_t H, int64_t W, int64_t D,
+                                      const int64_t* l_strides, const int64_t* r_strides,
+                                      void* stream) {
+  SM_ENTRY_BEGIN
+  return dot_volume_valu_entry(left, right, out, dtype, N, C, H, W, D, 1, l_strides, r_strides,
+                               1, stream);
+}
+
+extern "C" int sm_cv_groupwise(const void* left, const void* right, float* out, int dtype,
+                               int64_t N, int64_t C, int64_t H, int64_t W, int64_t D, int64_t G,
+                               const int64_t* l_strides, const int64_t* r_strides,
+                               void* stream) {
+  SM_ENTRY_BEGIN
+  return dot_volume_valu_entry(left, right, out, dtype, N, C, H, W, D, G, l_strides, r_strides,
+                               2, stream);
+}
+
+extern "C" int sm_cv_concat(const void* left, const void* right, void* out, int dtype, int64_t N,
+                            int64_t C, int64_t H, int64_t W, int64_t D,
+                            const int64_t* l_strides, const int64_t* r_strides, void* stream) {
+  SM_ENTRY_BEGIN
+  return concat_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, stream);
+}
+
+extern "C" int sm_cv_interweave(const void* left, const void* right, void* out, int dtype,
+                                int64_t N, int64_t C, int64_t H, int64_t W,
+                                const int64_t* l_strides, const int64_t* r_strides,
+                                void* stream) {
+  SM_ENTRY_BEGIN
+  return interweave_entry(left, right, out, dtype, N, C, H, W, l_strides, r_strides, stream);
+}
+
+extern "C" int sm_cv_interweave_shifted(const void* left, const void* right, void* out,
+                                        int dtype, int64_t N, int64_t C, int64_t H, int64_t W,
+                                        int64_t D, const int64_t* l_strides,
+                                        const int64_t* r_strides, void* stream) {
+  SM_ENTRY_BEGIN
+  return shifted_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0, stream);
+}
+
+extern "C" int sm_cv_diff(const void* left, const void* right, void* out, int dtype, int64_t N,
+                          int64_t C, int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
+                          const int64_t* r_strides, void* stream) {
+  SM_ENTRY_BEGIN
+  return shifted_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 1, stream);
+}
+
+extern "C" int sm_regress_softargmin(const void* volume, void* out, int dtype, int64_t N,
+                                     int64_t D, int64_t H, int64_t W, int flags,
+                                     const int64_t* vol_strides, void* stream) {
+  SM_ENTRY_BEGIN
+  return softargmin_entry(volume, out, dtype, N, D, H, W, flags, vol_strides, stream);
+}
+
+extern "C" int sm_regress_argext(const void* volume, int64_t* out, int dtype, int64_t N,
+                                 int64_t D, int64_t H, int64_t W, int mode,
+                                 const int64_t* vol_strides, void* stream) {
+  SM_ENTRY_BEGIN
+  return argext_entry(volume, out, dtype, N, D, H, W, mode, vol_strides, stream);
+}

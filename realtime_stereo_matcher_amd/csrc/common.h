@@ -1,0 +1,79 @@
+// Shared helpers for the gfx950 stereo cost-volume kernels: dtype traits, feature-map
+// views, argument validation and the thread-local error string of the C ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/stereocv.h"
+
+namespace smcv {
+
+// ------------------------------------------------------------------------------- errors
+std::string& last_error();
+int fail(int code, const std::string& msg);
+int check_launch(const char* what);
+
+// ------------------------------------------------------------------------------- dtypes
+// Storage scalars.  bf16 is handled as raw 16-bit patterns with explicit RNE rounding so
+// the conversion is identical to torch's (round-to-nearest-even, NaN stays NaN).
+struct bf16_t { uint16_t bits; };
+
+template <typename T> struct io;
+template <> struct io<float> {
+  static __device__ __forceinline__ float to_f(float v) { return v; }
+  static __device__ __forceinline__ float from_f(float v) { return v; }
+};
+template <> struct io<__half> {
+  static __device__ __forceinline__ float to_f(__half v) { return __half2float(v); }
+  static __device__ __forceinline__ __half from_f(float v) { return __float2half_rn(v); }
+};
+template <> struct io<bf16_t> {
+  static __device__ __forceinline__ float to_f(bf16_t v) {
+    return __uint_as_float(static_cast<uint32_t>(v.bits) << 16);
+  }
+  static __device__ __forceinline__ bf16_t from_f(float v) {
+    uint32_t u = __float_as_uint(v);
+    bf16_t r;
+    if ((u & 0x7fffffffu) > 0x7f800000u) {
+      r.bits = static_cast<uint16_t>((u >> 16) | 0x0040u);  // quiet NaN, sign kept
+    } else {
+      r.bits = static_cast<uint16_t>((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+    }
+    return r;
+  }
+};
+
+template <typename T> __device__ __forceinline__ float to_f(T v) { return io<T>::to_f(v); }
+template <typename T> __device__ __forceinline__ T from_f(float v) { return io<T>::from_f(v); }
+
+inline int elem_size(int dtype) { return dtype == SM_F32 ? 4 : 2; }
+inline bool valid_dtype(int dtype) { return dtype == SM_F32 || dtype == SM_F16 || dtype == SM_BF16; }
+
+// ------------------------------------------------------------------------------- views
+// Element strides of an (N, C, H, W) feature map; W stride is 1 by contract.
+struct Strides4 {
+  int64_t n, c, h;
+};
+
+int read_strides(const int64_t* s, int64_t C, int64_t H, int64_t W, Strides4* out,
+                 const char* name);
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace smcv
+
+// Dispatch a templated body on the runtime dtype code.
+#define SM_DISPATCH_DTYPE(dtype, T, ...)                                   \
+  switch (dtype) {                                                         \
+    case SM_F32: { using T = float; __VA_ARGS__; } break;                  \
+    case SM_F16: { using T = __half; __VA_ARGS__; } break;                 \
+    case SM_BF16: { using T = ::smcv::bf16_t; __VA_ARGS__; } break;        \
+    default: return ::smcv::fail(SM_EDTYPE, "unsupported dtype code");     \
+  }

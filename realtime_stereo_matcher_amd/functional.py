@@ -1,0 +1,315 @@
+"""Functional front-end of the MI355X stereo cost-volume engine.
+
+Every function validates its arguments the way the reference does, allocates the output
+with the caching allocator on the input's device and enqueues ONE libstereocv kernel on
+the current HIP stream (no host sync).  There is no CPU / eager fallback: tensors must live
+on a HIP device and the native library must load, otherwise the call raises.
+
+Reference operators mirrored (babiking/realtime_stereo_matcher):
+  inner_product_volume   cost_volume/inner_product.py:11-42
+  groupwise_volume       cost_volume/groupwise.py:24-56
+  concat_volume          cost_volume/concatenate.py:11-41
+  interweave             cost_volume/interweave.py:10-22, model/mobile_stereo_net_v4.py:17-23
+  interweave_volume      model/mobile_stereo_net_v4.py:443-461 (shifted interweave, materialised)
+  difference_volume      model/mobile_stereo_net.py:8-27 (+ _v2.py:8-27, _v3.py:9-28)
+  correlation_volume     model/mobile_disp_net_c.py:188-205
+  soft_argmin            model/mobile_disp_net_c.py:208-220, model/mobile_stereo_net.py:144-147
+  regression_presoftmax  model/mobile_stereo_net_v4.py:10-14
+  hard_argmin/argmax     build-defined
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+_DTYPES = {torch.float32: _lib.SM_F32, torch.float16: _lib.SM_F16, torch.bfloat16: _lib.SM_BF16}
+_ALGOS = {"auto": _lib.SM_IP_AUTO, "valu": _lib.SM_IP_VALU, "mfma": _lib.SM_IP_MFMA_F32}
+
+
+# ----------------------------------------------------------------------------------- plumbing
+def _device_check(*ts):
+    dev = ts[0].device
+    for t in ts:
+        if t.device.type != "cuda":
+            raise RuntimeError(
+                "realtime_stereo_matcher_amd runs on HIP devices only (got a tensor on "
+                f"'{t.device}'); there is no CPU fallback -- move the features with .cuda()")
+        if t.device != dev:
+            raise RuntimeError(f"tensors on different devices: {dev} vs {t.device}")
+    return dev
+
+
+def _dtype_code(t):
+    code = _DTYPES.get(t.dtype)
+    if code is None:
+        raise TypeError(f"unsupported dtype {t.dtype}; expected float32, float16 or bfloat16")
+    return code
+
+
+def _rows_contiguous(t):
+    """The C ABI needs unit W stride; any other stride pattern is passed through."""
+    return t if (t.dim() == 0 or t.stride(-1) == 1 or t.size(-1) <= 1) else t.contiguous()
+
+
+def _stride_ok(t):
+    # size-1 W can carry any stride in torch; normalise so the ABI sees 1
+    if t.size(-1) <= 1 and t.stride(-1) != 1:
+        t = t.contiguous()
+    return t
+
+
+def _pair(left, right, what):
+    if not isinstance(left, torch.Tensor) or not isinstance(right, torch.Tensor):
+        raise TypeError(f"{what}: left and right must be tensors")
+    if left.dim() != 4 or right.dim() != 4:
+        raise RuntimeError(f"{what}: expected 4-D (N, C, H, W) features, got {tuple(left.shape)} "
+                           f"and {tuple(right.shape)}")
+    if left.shape != right.shape:
+        raise RuntimeError(f"{what}: left/right shape mismatch {tuple(left.shape)} vs "
+                           f"{tuple(right.shape)}")
+    if left.dtype != right.dtype:
+        raise RuntimeError(f"{what}: left/right dtype mismatch {left.dtype} vs {right.dtype}")
+    code = _dtype_code(left)
+    dev = _device_check(left, right)
+    left = _stride_ok(_rows_contiguous(left))
+    right = _stride_ok(_rows_contiguous(right))
+    return left, right, dev, code
+
+
+def _stream(dev):
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def _disp(max_disparity, what):
+    d = int(max_disparity)
+    if d < 0:
+        raise RuntimeError(f"{what}: max disparity must be non-negative, got {d}")
+    return d
+
+
+class _ForwardOnly(torch.autograd.Function):
+    """Marks outputs as produced by a forward-only native kernel (no autograd support yet)."""
+
+    @staticmethod
+    def forward(ctx, fn, *tensors):
+        return fn()
+
+    @staticmethod
+    def backward(ctx, *grads):
+        raise NotImplementedError(
+            "realtime_stereo_matcher_amd cost-volume kernels are forward/inference-only; "
+            "backward is not implemented")
+
+
+def _run(fn, *inputs):
+    if torch.is_grad_enabled() and any(t.requires_grad for t in inputs):
+        return _ForwardOnly.apply(fn, *inputs)
+    return fn()
+
+
+def _ptr(t):
+    return t.data_ptr()
+
+
+# ----------------------------------------------------------------------------- a-1, a-6, a-2
+def inner_product_volume(left, right, max_disparity, algo="auto"):
+    """(N,C,H,W) x2 -> (N,D,H,W): sum_c L*R(x-d) for x >= d, 0 elsewhere (left dtype/device)."""
+    left, right, dev, code = _pair(left, right, "inner_product_volume")
+    D = _disp(max_disparity, "inner_product_volume")
+    if algo not in _ALGOS:
+        raise ValueError(f"algo must be one of {sorted(_ALGOS)}")
+    n, c, h, w = left.shape
+
+    def fn():
+        out = torch.empty((n, D, h, w), dtype=left.dtype, device=dev)
+        if out.numel():
+            lib = _lib.load()
+            _lib.check(lib.sm_cv_inner_product_ex(
+                _ptr(left), _ptr(right), _ptr(out), code, n, c, h, w, D,
+                _lib.strides_arg(left), _lib.strides_arg(right), _ALGOS[algo], _stream(dev)),
+                "sm_cv_inner_product")
+        return out
+
+    return _run(fn, left, right)
+
+
+def correlation_volume(l_fmap, r_fmap, max_disp):
+    """(N,C,H,W) x2 -> (N,D,H,W): mean_c L*R(x-d) for x >= d, 0 elsewhere."""
+    left, right, dev, code = _pair(l_fmap, r_fmap, "correlation_volume")
+    D = _disp(max_disp, "correlation_volume")
+    n, c, h, w = left.shape
+
+    def fn():
+        out = torch.empty((n, D, h, w), dtype=left.dtype, device=dev)
+        if out.numel():
+            lib = _lib.load()
+            _lib.check(lib.sm_cv_correlation_mean(
+                _ptr(left), _ptr(right), _ptr(out), code, n, c, h, w, D,
+                _lib.strides_arg(left), _lib.strides_arg(right), _stream(dev)),
+                "sm_cv_correlation_mean")
+        return out
+
+    return _run(fn, left, right)
+
+
+def groupwise_volume(left, right, n_groups, max_disparity):
+    """(N,C,H,W) x2 -> (N,G,H,W,D) float32: per-group mean of L*R(x-d), 0 for x < d.
+
+    Deviation (documented): the reference allocates its output on the CPU regardless of the
+    input device (cost_volume/groupwise.py:39); this engine returns it on the input device.
+    """
+    G = int(n_groups)
+    D = _disp(max_disparity, "groupwise_volume")
+    if isinstance(left, torch.Tensor) and left.dim() == 4 and D > 0:
+        # the reference asserts inside groupwise(), reached once per disparity (groupwise.py:15-17)
+        c = left.shape[1]
+        assert c % G == 0, f"groupwise cost channel ({c}) % #groups ({G}) != 0."
+    left, right, dev, code = _pair(left, right, "groupwise_volume")
+    n, c, h, w = left.shape
+
+    def fn():
+        out = torch.empty((n, G, h, w, D), dtype=torch.float32, device=dev)
+        if out.numel():
+            lib = _lib.load()
+            _lib.check(lib.sm_cv_groupwise(
+                _ptr(left), _ptr(right), _ptr(out), code, n, c, h, w, D, G,
+                _lib.strides_arg(left), _lib.strides_arg(right), _stream(dev)),
+                "sm_cv_groupwise")
+        return out
+
+    return _run(fn, left, right)
+
+
+# ----------------------------------------------------------------------------- a-3, a-4, a-5
+def concat_volume(left, right, max_disparity):
+    """(N,C,H,W) x2 -> (N,2C,H,W,D): [:C]=L, [C:]=R(x-d) for x >= d, 0 elsewhere (bit-exact)."""
+    left, right, dev, code = _pair(left, right, "concat_volume")
+    D = _disp(max_disparity, "concat_volume")
+    n, c, h, w = left.shape
+
+    def fn():
+        out = torch.empty((n, 2 * c, h, w, D), dtype=left.dtype, device=dev)
+        if out.numel():
+            lib = _lib.load()
+            _lib.check(lib.sm_cv_concat(
+                _ptr(left), _ptr(right), _ptr(out), code, n, c, h, w, D,
+                _lib.strides_arg(left), _lib.strides_arg(right), _stream(dev)), "sm_cv_concat")
+        return out
+
+    return _run(fn, left, right)
+
+
+def interweave(left, right):
+    """(N,C,H,W) x2 -> (N,2C,H,W): even channels L, odd channels R (bit-exact)."""
+    left, right, dev, code = _pair(left, right, "interweave")
+    n, c, h, w = left.shape
+
+    def fn():
+        out = torch.empty((n, 2 * c, h, w), dtype=left.dtype, device=dev)
+        if out.numel():
+            lib = _lib.load()
+            _lib.check(lib.sm_cv_interweave(
+                _ptr(left), _ptr(right), _ptr(out), code, n, c, h, w,
+                _lib.strides_arg(left), _lib.strides_arg(right), _stream(dev)), "sm_cv_interweave")
+        return out
+
+    return _run(fn, left, right)
+
+
+def interweave_volume(left, right, max_disparity):
+    """(N,C,H,W) x2 -> (N,2C,D,H,W): the v4 per-disparity interweave, 0 for x < d (bit-exact)."""
+    left, right, dev, code = _pair(left, right, "interweave_volume")
+    D = _disp(max_disparity, "interweave_volume")
+    n, c, h, w = left.shape
+
+    def fn():
+        out = torch.empty((n, 2 * c, D, h, w), dtype=left.dtype, device=dev)
+        if out.numel():
+            lib = _lib.load()
+            _lib.check(lib.sm_cv_interweave_shifted(
+                _ptr(left), _ptr(right), _ptr(out), code, n, c, h, w, D,
+                _lib.strides_arg(left), _lib.strides_arg(right), _stream(dev)),
+                "sm_cv_interweave_shifted")
+        return out
+
+    return _run(fn, left, right)
+
+
+def difference_volume(left, right, max_disp):
+    """(N,C,H,W) x2 -> (N,C,D,H,W): L - R(x-d) for x >= d, 1.0 elsewhere (bit-exact)."""
+    left, right, dev, code = _pair(left, right, "difference_volume")
+    D = _disp(max_disp, "difference_volume")
+    n, c, h, w = left.shape
+
+    def fn():
+        out = torch.empty((n, c, D, h, w), dtype=left.dtype, device=dev)
+        if out.numel():
+            lib = _lib.load()
+            _lib.check(lib.sm_cv_diff(
+                _ptr(left), _ptr(right), _ptr(out), code, n, c, h, w, D,
+                _lib.strides_arg(left), _lib.strides_arg(right), _stream(dev)), "sm_cv_diff")
+        return out
+
+    return _run(fn, left, right)
+
+
+# ----------------------------------------------------------------------------- a-7, a-8
+def _volume(volume, what):
+    if not isinstance(volume, torch.Tensor):
+        raise TypeError(f"{what}: volume must be a tensor")
+    if volume.dim() != 4:
+        raise RuntimeError(f"{what}: expected a 4-D (N, D, H, W) volume, got {tuple(volume.shape)}")
+    code = _dtype_code(volume)
+    dev = _device_check(volume)
+    return _stride_ok(_rows_contiguous(volume)), dev, code
+
+
+def _regress(volume, flags, what):
+    vol, dev, code = _volume(volume, what)
+    n, d, h, w = vol.shape
+
+    def fn():
+        out = torch.empty((n, h, w), dtype=vol.dtype, device=dev)
+        if out.numel():
+            lib = _lib.load()
+            _lib.check(lib.sm_regress_softargmin(
+                _ptr(vol), _ptr(out), code, n, d, h, w, flags, _lib.strides_arg(vol), _stream(dev)),
+                "sm_regress_softargmin")
+        return out
+
+    return _run(fn, vol)
+
+
+def soft_argmin(volume, keepdim=True):
+    """sum_d d * softmax_d(volume) -> (N,1,H,W) (keepdim) or (N,H,W); fp64 accumulation."""
+    out = _regress(volume, _lib.SM_REGRESS_SOFTMAX, "soft_argmin")
+    return out.unsqueeze(1) if keepdim else out
+
+
+def regression_presoftmax(prob):
+    """sum_d d * prob[:, d] over an already-softmaxed (N,D,H,W) volume -> (N,H,W)."""
+    return _regress(prob, _lib.SM_REGRESS_PRESOFTMAXED, "regression_presoftmax")
+
+
+def _argext(volume, mode, what):
+    vol, dev, code = _volume(volume, what)
+    n, d, h, w = vol.shape
+    if d == 0 and n * h * w > 0:
+        raise IndexError(f"{what}: cannot reduce over an empty disparity axis")
+    out = torch.empty((n, h, w), dtype=torch.int64, device=dev)
+    if out.numel():
+        lib = _lib.load()
+        _lib.check(lib.sm_regress_argext(_ptr(vol), _ptr(out), code, n, d, h, w, mode,
+                                         _lib.strides_arg(vol), _stream(dev)), "sm_regress_argext")
+    return out
+
+
+def hard_argmin(volume):
+    """First index of the minimum over D -> (N,H,W) int64 (ties -> lowest d, NaN wins)."""
+    return _argext(volume, _lib.SM_ARGMIN, "hard_argmin")
+
+
+def hard_argmax(volume):
+    """First index of the maximum over D -> (N,H,W) int64 (ties -> lowest d, NaN wins)."""
+    return _argext(volume, _lib.SM_ARGMAX, "hard_argmax")

@@ -1,0 +1,2 @@
+"""Hot-path helpers of ``model/mobile_stereo_net_v2.py`` (same ops as v1: :8-27, :217-220)."""
+from .mobile_stereo_net import make_cost_volume, soft_argmin_regression  # noqa: F401

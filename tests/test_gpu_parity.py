@@ -1,0 +1,389 @@
+"""GPU parity of the HIP kernels (through the C ABI) against the golden vectors recorded from
+the reference and against the CPU oracle (oracle/stereo_oracle.py).
+
+Tolerances (north star, BASELINE.json): fp32 volumes / regression within 1e-4 absolute;
+copy volumes (concat, interweave, difference) and argmin/argmax indices bit-exact.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import cases, load_case
+from oracle import stereo_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+TDT = {"f32": torch.float32, "f16": torch.float16, "bf16": torch.bfloat16}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+def dev(a, dt="f32"):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to("cuda").to(TDT[dt])
+
+
+def host(t):
+    return t.float().cpu().numpy() if t.dtype != torch.int64 else t.cpu().numpy()
+
+
+def _ids(cs):
+    return [c["name"] for c in cs]
+
+
+# =============================================================================== golden vectors
+@pytest.mark.parametrize("algo", ["auto", "valu"])
+@pytest.mark.parametrize("rec", cases("inner_product"), ids=_ids(cases("inner_product")))
+def test_golden_inner_product(rec, algo):
+    from realtime_stereo_matcher_amd.cost_volume import TorchInnerProductCost
+
+    a = load_case(rec)
+    dt = rec["dtype"]
+    D = rec["params"]["max_disparity"]
+    L, R = dev(a["left"], dt), dev(a["right"], dt)
+    if "noncontig" in rec["name"]:
+        L = L.transpose(2, 3).contiguous().transpose(2, 3)  # W stride != 1 -> wrapper re-lays rows
+    out = TorchInnerProductCost(D, algo=algo)(L, R)
+    assert out.shape == a["out"].shape and out.dtype == TDT[dt] and out.device == L.device
+    got = host(out)
+    if rec.get("exact"):
+        np.testing.assert_array_equal(got, a["out"])
+    elif dt == "f32":
+        np.testing.assert_allclose(got, a["out"], atol=TOL, rtol=0)
+    else:
+        # fp32 accumulation of exact products vs torch's per-product rounding: compare with
+        # the exact-product oracle to one output ulp, and with the literal golden loosely.
+        ref = O.inner_product(a["left"], a["right"], D, out_dtype=dt).astype(np.float32)
+        ulp = 2.0 ** -10 if dt == "f16" else 2.0 ** -7
+        np.testing.assert_allclose(got, ref, rtol=ulp, atol=1e-3)
+        np.testing.assert_allclose(got, a["out"], rtol=4 * ulp, atol=4e-2)
+
+
+@pytest.mark.parametrize("rec", cases("correlation"), ids=_ids(cases("correlation")))
+def test_golden_correlation(rec):
+    from realtime_stereo_matcher_amd.model.mobile_disp_net_c import make_correlation_volume
+
+    a = load_case(rec)
+    out = make_correlation_volume(dev(a["left"]), dev(a["right"]), rec["params"]["max_disp"])
+    np.testing.assert_allclose(host(out), a["out"], atol=TOL, rtol=0)
+
+
+@pytest.mark.parametrize("rec", cases("groupwise"), ids=_ids(cases("groupwise")))
+def test_golden_groupwise(rec):
+    from realtime_stereo_matcher_amd.cost_volume import TorchGroupwiseCost
+
+    a = load_case(rec)
+    p = rec["params"]
+    dt = rec["dtype"]
+    out = TorchGroupwiseCost(p["n_groups"], p["max_disparity"])(dev(a["left"], dt), dev(a["right"], dt))
+    assert out.dtype == torch.float32 and out.shape == a["out"].shape
+    got = host(out)
+    if dt == "f32":
+        np.testing.assert_allclose(got, a["out"], atol=TOL, rtol=0)
+    else:
+        # parity bar: the fp32 oracle on the same bf16-representable inputs
+        ref = O.groupwise(a["left"], a["right"], p["n_groups"], p["max_disparity"])
+        np.testing.assert_allclose(got, ref, atol=TOL, rtol=0)
+        # the reference's literal bf16 product/mean rounding differs by <= 2 bf16 ulp
+        np.testing.assert_allclose(got, a["out"], rtol=2 * 2.0 ** -7, atol=1e-6)
+
+
+@pytest.mark.parametrize("rec", cases("concat"), ids=_ids(cases("concat")))
+def test_golden_concat(rec):
+    from realtime_stereo_matcher_amd.cost_volume import TorchConcatenateCost
+
+    a = load_case(rec)
+    dt = rec["dtype"]
+    out = TorchConcatenateCost(rec["params"]["max_disparity"])(dev(a["left"], dt), dev(a["right"], dt))
+    np.testing.assert_array_equal(host(out), a["out"].astype(np.float32))
+
+
+@pytest.mark.parametrize("rec", cases("interweave"), ids=_ids(cases("interweave")))
+def test_golden_interweave(rec):
+    from realtime_stereo_matcher_amd.cost_volume import TorchInterweaveCost
+    from realtime_stereo_matcher_amd.model.mobile_stereo_net_v4 import interweave_tensors
+
+    a = load_case(rec)
+    dt = rec["dtype"]
+    L, R = dev(a["left"], dt), dev(a["right"], dt)
+    np.testing.assert_array_equal(host(TorchInterweaveCost()(L, R)), a["out"].astype(np.float32))
+    np.testing.assert_array_equal(host(interweave_tensors(L, R)), a["out"].astype(np.float32))
+
+
+@pytest.mark.parametrize("rec", cases("interweave_shifted"), ids=_ids(cases("interweave_shifted")))
+def test_golden_interweave_shifted(rec):
+    from realtime_stereo_matcher_amd.model.mobile_stereo_net_v4 import interweave_volume
+
+    a = load_case(rec)
+    dt = rec["dtype"]
+    out = interweave_volume(dev(a["left"], dt), dev(a["right"], dt), rec["params"]["max_disparity"])
+    np.testing.assert_array_equal(host(out), a["out"].astype(np.float32))
+
+
+@pytest.mark.parametrize("rec", cases("diff_volume"), ids=_ids(cases("diff_volume")))
+def test_golden_diff_volume(rec):
+    from realtime_stereo_matcher_amd.model.mobile_stereo_net import make_cost_volume
+
+    a = load_case(rec)
+    dt = rec["dtype"]
+    out = make_cost_volume(dev(a["left"], dt), dev(a["right"], dt), rec["params"]["max_disp"])
+    np.testing.assert_array_equal(host(out), a["out"].astype(np.float32))
+
+
+@pytest.mark.parametrize("rec", cases("softargmin"), ids=_ids(cases("softargmin")))
+def test_golden_softargmin(rec):
+    from realtime_stereo_matcher_amd.model.mobile_disp_net_c import disparity_regression
+    from realtime_stereo_matcher_amd.model.mobile_stereo_net import soft_argmin_regression
+
+    a = load_case(rec)
+    v = dev(a["volume"])
+    for out in (disparity_regression(v, rec["params"]["max_disp"]), soft_argmin_regression(v)):
+        assert out.shape == a["out"].shape
+        np.testing.assert_allclose(host(out), a["out"], atol=TOL, rtol=0)
+        np.testing.assert_allclose(host(out), O.softargmin(a["volume"]), atol=2e-5, rtol=0)
+
+
+@pytest.mark.parametrize("rec", cases("regression_presoftmax"), ids=_ids(cases("regression_presoftmax")))
+def test_golden_regression_presoftmax(rec):
+    from realtime_stereo_matcher_amd.model.mobile_stereo_net_v4 import disparity_regression
+
+    a = load_case(rec)
+    out = disparity_regression(dev(a["volume"]), rec["params"]["maxdisp"])
+    assert out.shape == a["out"].shape
+    np.testing.assert_allclose(host(out), a["out"], atol=TOL, rtol=0)
+
+
+@pytest.mark.parametrize("rec", cases("argext"), ids=_ids(cases("argext")))
+def test_golden_argext(rec):
+    from realtime_stereo_matcher_amd import functional as F
+    from realtime_stereo_matcher_amd.cost_volume import TorchInnerProductCost
+
+    a = load_case(rec)
+    fn = F.hard_argmax if rec["params"]["mode"] == "max" else F.hard_argmin
+    np.testing.assert_array_equal(host(fn(dev(a["volume"]))), a["out"])
+    if "left" in a:  # end to end: integer features -> exact volume -> bit-exact argmax
+        for algo in ("auto", "valu"):
+            vol = TorchInnerProductCost(rec["params"]["max_disparity"], algo=algo)(dev(a["left"]), dev(a["right"]))
+            np.testing.assert_array_equal(host(vol), a["volume"])
+            np.testing.assert_array_equal(host(F.hard_argmax(vol)), a["out"])
+
+
+# =============================================================================== oracle sweeps
+SHAPES = [  # (N, C, H, W, D)
+    (1, 1, 1, 1, 1), (1, 3, 2, 7, 5), (2, 17, 3, 65, 24), (1, 64, 2, 200, 192), (1, 16, 3, 130, 256),
+    (1, 32, 2, 100, 300), (1, 8, 2, 64, 64), (1, 5, 1, 33, 0), (3, 64, 1, 97, 65), (1, 128, 2, 70, 48),
+]
+
+
+def _feats(seed, shape, kind="normal"):
+    rng = np.random.default_rng(seed)
+    if kind == "int":
+        return (rng.integers(-8, 9, size=shape).astype(np.float32),
+                rng.integers(-8, 9, size=shape).astype(np.float32))
+    return rng.standard_normal(shape, dtype=np.float32), rng.standard_normal(shape, dtype=np.float32)
+
+
+@pytest.mark.parametrize("algo", ["auto", "valu"])
+@pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
+def test_inner_product_vs_oracle(shape, algo):
+    from realtime_stereo_matcher_amd import functional as F
+
+    n, c, h, w, D = shape
+    l, r = _feats(hash(shape) % 1000, (n, c, h, w))
+    got = host(F.inner_product_volume(dev(l), dev(r), D, algo=algo))
+    np.testing.assert_allclose(got, O.inner_product(l, r, D), atol=TOL * max(1, c / 64), rtol=0)
+    li, ri = _feats(7, (n, c, h, w), "int")
+    np.testing.assert_array_equal(host(F.inner_product_volume(dev(li), dev(ri), D, algo=algo)),
+                                  O.inner_product(li, ri, D))
+
+
+@pytest.mark.parametrize("shape", SHAPES[:7], ids=[str(s) for s in SHAPES[:7]])
+def test_correlation_and_groupwise_vs_oracle(shape):
+    from realtime_stereo_matcher_amd import functional as F
+
+    n, c, h, w, D = shape
+    l, r = _feats(11, (n, c, h, w))
+    np.testing.assert_allclose(host(F.correlation_volume(dev(l), dev(r), D)),
+                               O.correlation_mean(l, r, D), atol=TOL, rtol=0)
+    for G in {1, c} | ({c // 2} if c % 2 == 0 else set()):
+        got = host(F.groupwise_volume(dev(l), dev(r), G, D))
+        np.testing.assert_allclose(got, O.groupwise(l, r, G, D), atol=TOL, rtol=0)
+
+
+@pytest.mark.parametrize("dt", ["f32", "f16", "bf16"])
+@pytest.mark.parametrize("shape", [(1, 3, 2, 7, 5), (2, 5, 3, 33, 40), (1, 4, 2, 64, 64), (1, 6, 2, 19, 8)])
+def test_copy_volumes_vs_oracle(shape, dt):
+    from realtime_stereo_matcher_amd import functional as F
+
+    n, c, h, w, D = shape
+    l, r = _feats(3, (n, c, h, w))
+    l, r = O.round_to_dtype(l, dt).astype(np.float32), O.round_to_dtype(r, dt).astype(np.float32)
+    L, R = dev(l, dt), dev(r, dt)
+    np.testing.assert_array_equal(host(F.concat_volume(L, R, D)), O.concatenate(l, r, D))
+    np.testing.assert_array_equal(host(F.interweave(L, R)), O.interweave(l, r))
+    np.testing.assert_array_equal(host(F.interweave_volume(L, R, D)), O.interweave_shifted(l, r, D))
+    want = O.round_to_dtype(O.diff_volume(l, r, D), dt).astype(np.float32) if dt != "f32" else O.diff_volume(l, r, D)
+    np.testing.assert_array_equal(host(F.difference_volume(L, R, D)), want)
+
+
+def test_noncontiguous_inputs():
+    """Strided (but row-contiguous) views go through the strides of the C ABI untouched."""
+    from realtime_stereo_matcher_amd import functional as F
+
+    l, r = _feats(5, (2, 24, 6, 40))
+    L, R = dev(l), dev(r)
+    Ls, Rs = L[:, ::2, 1::2], R[:, ::2, 1::2]  # channel and row strides
+    ls, rs = l[:, ::2, 1::2], r[:, ::2, 1::2]
+    np.testing.assert_allclose(host(F.inner_product_volume(Ls, Rs, 17)), O.inner_product(ls, rs, 17), atol=TOL)
+    np.testing.assert_allclose(host(F.correlation_volume(Ls, Rs, 9)), O.correlation_mean(ls, rs, 9), atol=TOL)
+    np.testing.assert_allclose(host(F.groupwise_volume(Ls, Rs, 3, 9)), O.groupwise(ls, rs, 3, 9), atol=TOL)
+    np.testing.assert_array_equal(host(F.concat_volume(Ls, Rs, 7)), O.concatenate(ls, rs, 7))
+    np.testing.assert_array_equal(host(F.interweave(Ls, Rs)), O.interweave(ls, rs))
+    np.testing.assert_array_equal(host(F.difference_volume(Ls, Rs, 7)), O.diff_volume(ls, rs, 7))
+    vol = dev(np.random.default_rng(1).standard_normal((2, 30, 5, 12), dtype=np.float32))
+    vs = vol[:, :, ::2]
+    np.testing.assert_allclose(host(F.soft_argmin(vs)), O.softargmin(host(vs)), atol=2e-5)
+    np.testing.assert_array_equal(host(F.hard_argmin(vs)), O.argext(host(vs), "min"))
+
+
+@pytest.mark.parametrize("shape", [(1, 192, 3, 257), (2, 24, 5, 7), (1, 1, 2, 3), (1, 300, 2, 64), (1, 48, 1, 1000)])
+@pytest.mark.parametrize("scale", [1.0, 30.0])
+def test_regression_vs_oracle(shape, scale):
+    from realtime_stereo_matcher_amd import functional as F
+
+    v = np.random.default_rng(9).standard_normal(shape, dtype=np.float32) * scale
+    V = dev(v)
+    np.testing.assert_allclose(host(F.soft_argmin(V, keepdim=False)), O.softargmin(v, keepdim=False), atol=2e-5, rtol=0)
+    prob = torch.softmax(V, dim=1)
+    np.testing.assert_allclose(host(F.regression_presoftmax(prob)),
+                               O.regression_presoftmax(host(prob), shape[1]), atol=TOL, rtol=0)
+    vi = np.round(v).astype(np.float32)  # ties
+    for mode, fn in (("min", F.hard_argmin), ("max", F.hard_argmax)):
+        np.testing.assert_array_equal(host(fn(dev(vi))), O.argext(vi, mode))
+
+
+def test_regression_special_values():
+    from realtime_stereo_matcher_amd import functional as F
+
+    v = np.zeros((1, 20, 1, 6), np.float32)
+    v[0, :, 0, 0] = -np.inf                      # all -inf column -> NaN (torch)
+    v[0, 3, 0, 1] = np.nan                       # a NaN -> NaN; argmin/argmax pick it
+    v[0, :10, 0, 2] = -np.inf                    # leading -inf chunk then finite values
+    v[0, 5, 0, 3] = np.inf                       # +inf -> NaN in softmax
+    v[0, 7, 0, 4] = 80.0                         # large spread
+    t = torch.from_numpy(v)
+    ref = torch.sum(torch.softmax(t.double(), 1) * torch.arange(20.).view(1, -1, 1, 1), 1).float().numpy()
+    got = host(F.soft_argmin(dev(v), keepdim=False))
+    np.testing.assert_allclose(got, ref, atol=2e-5, equal_nan=True)
+    np.testing.assert_array_equal(host(F.hard_argmax(dev(v))), torch.argmax(t, 1).numpy())
+    np.testing.assert_array_equal(host(F.hard_argmin(dev(v))), torch.argmin(t, 1).numpy())
+
+
+def test_zero_channels_and_empty():
+    from realtime_stereo_matcher_amd import functional as F
+
+    z = torch.zeros(1, 0, 2, 9, device="cuda")
+    assert torch.equal(F.inner_product_volume(z, z, 4).cpu(), torch.zeros(1, 4, 2, 9))
+    corr = F.correlation_volume(z, z, 4).cpu()  # mean over empty C = NaN where x >= d
+    ref = torch.zeros(1, 4, 2, 9)
+    for d in range(4):
+        ref[:, d, :, d:] = float("nan")
+    assert torch.equal(torch.isnan(corr), torch.isnan(ref))
+    e = torch.zeros(0, 4, 2, 9, device="cuda")
+    assert F.inner_product_volume(e, e, 3).shape == (0, 3, 2, 9)
+    assert F.concat_volume(e, e, 3).shape == (0, 8, 2, 9, 3)
+
+
+# =============================================================================== full-size configs
+def _rows_check(full, fn_oracle, rows, atol, exact=False):
+    for y in rows:
+        want = fn_oracle(y)
+        got = host(full(y))
+        if exact:
+            np.testing.assert_array_equal(got, want)
+        else:
+            np.testing.assert_allclose(got, want, atol=atol, rtol=0)
+
+
+@pytest.mark.parametrize("algo", ["auto", "valu"])
+def test_cfg2_inner_product_full_size(algo):
+    """BASELINE configs[1]: 1x64x540x960 fp32, D=192 -- every row depends only on the same
+    row of L and R (inner_product.py:38-40), so rows sampled from the full-size launch are
+    compared with the oracle on the same rows; plus the soft-argmin of the full volume."""
+    from realtime_stereo_matcher_amd import functional as F
+
+    g = torch.Generator(device="cuda").manual_seed(0)
+    L = torch.randn(1, 64, 540, 960, device="cuda", generator=g)
+    R = torch.randn(1, 64, 540, 960, device="cuda", generator=g)
+    vol = F.inner_product_volume(L, R, 192, algo=algo)
+    disp = F.soft_argmin(vol)
+    torch.cuda.synchronize()
+    ln, rn = host(L), host(R)
+    for y in (0, 1, 269, 538, 539):
+        ref = O.inner_product(ln[:, :, y:y + 1], rn[:, :, y:y + 1], 192)
+        np.testing.assert_allclose(host(vol[:, :, y:y + 1]), ref, atol=TOL, rtol=0)
+        np.testing.assert_allclose(host(disp[:, :, y:y + 1]), O.softargmin(ref), atol=TOL, rtol=0)
+    # x < d triangle is exactly zero everywhere
+    tri = torch.arange(960, device="cuda")[None, :] < torch.arange(192, device="cuda")[:, None]
+    assert not vol[0].permute(1, 0, 2)[:, tri].any()
+
+
+def test_cfg3_groupwise_bf16_full_size():
+    """BASELINE configs[2]: 1x256x540x960 bf16, G=8, D=192, fp32 (N,G,H,W,D) output."""
+    from realtime_stereo_matcher_amd import functional as F
+
+    g = torch.Generator(device="cuda").manual_seed(0)
+    L = torch.randn(1, 256, 540, 960, device="cuda", generator=g).bfloat16()
+    R = torch.randn(1, 256, 540, 960, device="cuda", generator=g).bfloat16()
+    vol = F.groupwise_volume(L, R, 8, 192)
+    assert vol.shape == (1, 8, 540, 960, 192) and vol.dtype == torch.float32
+    ln, rn = host(L), host(R)
+    for y in (0, 300, 539):
+        ref = O.groupwise(ln[:, :, y:y + 1], rn[:, :, y:y + 1], 8, 192)
+        np.testing.assert_allclose(host(vol[:, :, y:y + 1]), ref, atol=TOL, rtol=0)
+
+
+def test_cfg4_correlation_full_res_pair():
+    """BASELINE configs[3] per pair: 16x1080x1920 fp32, D=256 (mean over C)."""
+    from realtime_stereo_matcher_amd import functional as F
+
+    g = torch.Generator(device="cuda").manual_seed(0)
+    L = torch.randn(1, 16, 1080, 1920, device="cuda", generator=g)
+    R = torch.randn(1, 16, 1080, 1920, device="cuda", generator=g)
+    vol = F.correlation_volume(L, R, 256)
+    ln, rn = host(L), host(R)
+    for y in (0, 777, 1079):
+        ref = O.correlation_mean(ln[:, :, y:y + 1], rn[:, :, y:y + 1], 256)
+        np.testing.assert_allclose(host(vol[:, :, y:y + 1]), ref, atol=TOL, rtol=0)
+
+
+def test_cfg5_concat_interweave_fp16_full_size():
+    """BASELINE configs[4]: 1x128x540x960 fp16, concat D=64 (17 GB) and interweave."""
+    from realtime_stereo_matcher_amd import functional as F
+
+    g = torch.Generator(device="cuda").manual_seed(0)
+    L = torch.randn(1, 128, 540, 960, device="cuda", generator=g).half()
+    R = torch.randn(1, 128, 540, 960, device="cuda", generator=g).half()
+    iw = F.interweave(L, R)
+    assert torch.equal(iw[:, 0::2], L) and torch.equal(iw[:, 1::2], R)
+    del iw
+    vol = F.concat_volume(L, R, 64)
+    assert vol.shape == (1, 256, 540, 960, 64)
+    ln, rn = host(L), host(R)
+    for y in (0, 123, 539):
+        ref = O.concatenate(ln[:, :, y:y + 1], rn[:, :, y:y + 1], 64)
+        np.testing.assert_array_equal(host(vol[:, :, y:y + 1]), ref)
+    # checksum of checksums: every d-slice of the left half sums to the shifted left plane
+    for d in (0, 17, 63):
+        assert torch.equal(vol[0, :128, :, d:, d], L[0, :, :, d:])
+        assert torch.equal(vol[0, 128:, :, d:, d], R[0, :, :, :960 - d])
+    del vol
+    sv = F.interweave_volume(L[:, :16], R[:, :16], 64)
+    for d in (0, 5, 63):
+        assert torch.equal(sv[0, 0::2, d, :, d:], L[0, :16, :, d:])
+        assert torch.equal(sv[0, 1::2, d, :, d:], R[0, :16, :, :960 - d])
+        assert not sv[0, :, d, :, :d].any()

@@ -1,0 +1,150 @@
+"""Pin the CPU oracle (oracle/stereo_oracle.py) and the eager CPU port (oracle/torch_port.py)
+against the golden vectors recorded from the reference's own modules (CPU-only tests)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import cases, load_case
+from oracle import stereo_oracle as O
+from oracle import torch_port as P
+
+TOL_F32 = 1e-4  # north-star fp32 bar (BASELINE.json)
+
+
+def _ids(cs):
+    return [c["name"] for c in cs]
+
+
+@pytest.mark.parametrize("rec", cases("inner_product"), ids=_ids(cases("inner_product")))
+def test_inner_product(rec):
+    a = load_case(rec)
+    D = rec["params"]["max_disparity"]
+    got = O.inner_product(a["left"], a["right"], D, out_dtype=rec["dtype"], literal=rec.get("literal", False))
+    ref = a["out"].astype(np.float32)
+    if rec.get("exact"):
+        np.testing.assert_array_equal(got, ref)
+    elif rec["dtype"] == "f32":
+        np.testing.assert_allclose(got, ref, atol=TOL_F32, rtol=0)
+    else:  # f16 / bf16: literal product rounding, fp64 sum -> within 1 output ulp
+        np.testing.assert_allclose(got.astype(np.float32), ref, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("rec", cases("groupwise"), ids=_ids(cases("groupwise")))
+def test_groupwise(rec):
+    a = load_case(rec)
+    p = rec["params"]
+    lit = "bf16" if rec["dtype"] == "bf16" else None
+    got = O.groupwise(a["left"], a["right"], p["n_groups"], p["max_disparity"], literal_dtype=lit)
+    assert got.dtype == np.float32 and got.shape == a["out"].shape
+    if lit:
+        # literal bf16 product + bf16 mean: agree within one bf16 ulp of the value
+        np.testing.assert_allclose(got, a["out"], rtol=2 ** -7, atol=1e-6)
+    else:
+        np.testing.assert_allclose(got, a["out"], atol=TOL_F32, rtol=0)
+
+
+def test_groupwise_assert_message(manifest):
+    with pytest.raises(AssertionError) as e:
+        O.groupwise(np.zeros((1, 16, 2, 8), np.float32), np.zeros((1, 16, 2, 8), np.float32), 3, 4)
+    assert str(e.value) == manifest["groupwise_assert_message_c16_g3"]
+
+
+@pytest.mark.parametrize("rec", cases("concat"), ids=_ids(cases("concat")))
+def test_concat(rec):
+    a = load_case(rec)
+    got = O.concatenate(a["left"], a["right"], rec["params"]["max_disparity"])
+    np.testing.assert_array_equal(got, a["out"])
+
+
+@pytest.mark.parametrize("rec", cases("interweave"), ids=_ids(cases("interweave")))
+def test_interweave(rec):
+    a = load_case(rec)
+    np.testing.assert_array_equal(O.interweave(a["left"], a["right"]), a["out"])
+
+
+@pytest.mark.parametrize("rec", cases("interweave_shifted"), ids=_ids(cases("interweave_shifted")))
+def test_interweave_shifted(rec):
+    a = load_case(rec)
+    got = O.interweave_shifted(a["left"], a["right"], rec["params"]["max_disparity"])
+    np.testing.assert_array_equal(got, a["out"])
+
+
+@pytest.mark.parametrize("rec", cases("diff_volume"), ids=_ids(cases("diff_volume")))
+def test_diff_volume(rec):
+    a = load_case(rec)
+    got = O.diff_volume(a["left"], a["right"], rec["params"]["max_disp"])
+    np.testing.assert_array_equal(got, a["out"])
+
+
+@pytest.mark.parametrize("rec", cases("correlation"), ids=_ids(cases("correlation")))
+def test_correlation(rec):
+    a = load_case(rec)
+    got = O.correlation_mean(a["left"], a["right"], rec["params"]["max_disp"])
+    np.testing.assert_allclose(got, a["out"], atol=TOL_F32, rtol=0)
+
+
+@pytest.mark.parametrize("rec", cases("softargmin"), ids=_ids(cases("softargmin")))
+def test_softargmin(rec):
+    a = load_case(rec)
+    got = O.softargmin(a["volume"], rec["params"]["max_disp"])
+    assert got.shape == a["out"].shape
+    np.testing.assert_allclose(got, a["out"], atol=TOL_F32, rtol=0)
+
+
+@pytest.mark.parametrize("rec", cases("regression_presoftmax"), ids=_ids(cases("regression_presoftmax")))
+def test_regression_presoftmax(rec):
+    a = load_case(rec)
+    got = O.regression_presoftmax(a["volume"], rec["params"]["maxdisp"])
+    assert got.shape == a["out"].shape
+    np.testing.assert_allclose(got, a["out"], atol=TOL_F32, rtol=0)
+
+
+def test_softargmin_assert_messages(manifest):
+    with pytest.raises(AssertionError) as e:
+        O.softargmin(np.zeros((1, 5, 2, 2), np.float32), 4)
+    assert str(e.value) == manifest["softargmin_assert_message_d5_vs_4"]
+    with pytest.raises(AssertionError) as e:
+        O.softargmin(np.zeros((5, 2, 2), np.float32), 5)
+    assert str(e.value) == manifest["softargmin_assert_message_ndim3"]
+
+
+@pytest.mark.parametrize("rec", cases("argext"), ids=_ids(cases("argext")))
+def test_argext(rec):
+    a = load_case(rec)
+    got = O.argext(a["volume"], rec["params"]["mode"])
+    np.testing.assert_array_equal(got, a["out"])
+    if "left" in a:  # the integer-valued volume itself is exact in the oracle
+        vol = O.inner_product(a["left"], a["right"], rec["params"]["max_disparity"])
+        np.testing.assert_array_equal(vol, a["volume"])
+
+
+def test_argext_nan_first_index():
+    v = np.zeros((1, 4, 1, 3), np.float32)
+    v[0, 2, 0, 0] = np.nan
+    v[0, 3, 0, 0] = np.nan
+    v[0, 1, 0, 1] = 5.0
+    t = torch.from_numpy(v)
+    for mode, fn in (("max", torch.argmax), ("min", torch.argmin)):
+        np.testing.assert_array_equal(O.argext(v, mode), fn(t, dim=1).numpy())
+
+
+# --------------------------------------------------------------------------- the eager CPU port
+def test_torch_port_inner_product_cfg1():
+    rec = next(c for c in cases("inner_product") if "cfg1" in c["name"])
+    a = load_case(rec)
+    got = P.sweep_dot_volume(torch.from_numpy(a["left"]), torch.from_numpy(a["right"]), 24)
+    np.testing.assert_allclose(got.numpy(), a["out"], atol=TOL_F32, rtol=0)
+
+
+@pytest.mark.parametrize("rec", cases("correlation"), ids=_ids(cases("correlation")))
+def test_torch_port_correlation(rec):
+    a = load_case(rec)
+    got = P.sweep_dot_volume(torch.from_numpy(a["left"]), torch.from_numpy(a["right"]),
+                             rec["params"]["max_disp"], mean=True)
+    np.testing.assert_allclose(got.numpy(), a["out"], atol=TOL_F32, rtol=0)
+
+
+@pytest.mark.parametrize("rec", cases("softargmin"), ids=_ids(cases("softargmin")))
+def test_torch_port_softargmin(rec):
+    a = load_case(rec)
+    np.testing.assert_array_equal(P.soft_argmin_eager(torch.from_numpy(a["volume"])).numpy(), a["out"])
