@@ -6,6 +6,9 @@ int dot_volume_valu_entry(const void* left, const void* right, void* out, int dt
                           int64_t C, int64_t H, int64_t W, int64_t D, int64_t G,
                           const int64_t* l_strides, const int64_t* r_strides, int mode,
                           void* stream);
+int band_mfma_entry(const void* left, const void* right, void* out, int dtype, int64_t N, int64_t C,
+                    int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
+                    const int64_t* r_strides, int mode, void* stream);
 int ip_mfma_entry(const void* left, const void* right, void* out, int dtype, int64_t N,
                   int64_t C, int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
                   const int64_t* r_strides, void* stream, bool* handled);
@@ -60,8 +63,7 @@ extern "C" int sm_cv_correlation_mean(const void* left, const void* right, void*
                                       const int64_t* l_strides, const int64_t* r_strides,
                                       void* stream) {
   SM_ENTRY_BEGIN
-  return dot_volume_valu_entry(left, right, out, dtype, N, C, H, W, D, 1, l_strides, r_strides,
-                               1, stream);
+  return band_mfma_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 1, stream);
 }
 
 extern "C" int sm_cv_groupwise(const void* left, const void* right, float* out, int dtype,
