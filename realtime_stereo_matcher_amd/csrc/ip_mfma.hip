@@ -50,6 +50,11 @@ __device__ __forceinline__ void load8(const T* __restrict__ rowp, int64_t cstrid
                                       int j, int W, float (&v)[8]) {
   const bool okj = (j >= 0) && (j < W);
   const int jc = min(max(j, 0), W - 1);
+  if (C <= 0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = 0.f;
+    return;
+  }
   if (cb + 8 <= C) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] = to_f(rowp[(int64_t)(cb + i) * cstride + jc]);
@@ -89,86 +94,155 @@ __device__ __forceinline__ void split8(const float (&v)[8], uint4 (&q)[P]) {
   if (P > 2) q[2] = l.u;
 }
 
+// 4 consecutive outputs (16-B aligned for fp32, 8-B for 16-bit types) in one store.
+template <typename T>
+__device__ __forceinline__ void store4(T* o, float4 v) {
+  if constexpr (sizeof(T) == 4) {
+    *reinterpret_cast<float4*>(o) = v;
+  } else {
+    union {
+      T e[4];
+      uint2 u;
+    } pk;
+    pk.e[0] = from_f<T>(v.x);
+    pk.e[1] = from_f<T>(v.y);
+    pk.e[2] = from_f<T>(v.z);
+    pk.e[3] = from_f<T>(v.w);
+    *reinterpret_cast<uint2*>(o) = pk.u;
+  }
+}
+
+// One unit of work: a 64-pixel segment of one image row and one pass of at most DMAX
+// disparities.  Consecutive work ids are the x-tiles of one row (they share right columns).
+struct BandWork {
+  int n, y, x0, dp, Dp, Tn, rwin, js;
+};
+
+__device__ __forceinline__ BandWork band_decode(int w, int tiles, int npass, int H, int D, int dmax) {
+  BandWork k;
+  const int pass = w % npass;
+  const int rest = w / npass;
+  const int tile = rest % tiles;
+  const int row = rest / tiles;
+  k.y = row % H;
+  k.n = row / H;
+  k.x0 = tile * kXT;
+  k.dp = pass * dmax;
+  k.Dp = min(dmax, D - k.dp);
+  k.Tn = 1 + (k.Dp - 1 + 15) / 16;       // 16x16 band blocks per x-block
+  k.rwin = kXT + 16 * (k.Tn - 1);        // right-window rows
+  k.js = k.x0 - k.dp - 16 * (k.Tn - 1);  // right column held in window row 0
+  return k;
+}
+
+// Persistent, software-pipelined band kernel.  Each workgroup walks a contiguous range of
+// work ids owned by its XCD group; the global loads of the NEXT (work, 32-channel step) are
+// issued into registers before the MFMAs and the epilogue of the current one, so HBM latency
+// hides behind compute and the output stream.
 template <typename T, int P, int TMAX>
 __global__ __launch_bounds__(kThreads, 2) void ip_band_mfma(
     const T* __restrict__ L, const T* __restrict__ R, T* __restrict__ out, int C, int H, int W,
-    int D, Strides4 ls, Strides4 rs, int divisor, int tiles, int nblocks) {
+    int D, Strides4 ls, Strides4 rs, int divisor, int tiles, int npass, int nwork) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int DMAX = 16 * (TMAX - 1);
+  constexpr int NR = (3 + TMAX) / 4;  // window staging items per thread = RWIN*4/256 at Tn=TMAX
 
-  // XCD-aware bijective remap: consecutive work ids (x-tiles of one row) share an XCD.
-  const int b = blockIdx.x;
-  const int q = nblocks >> 3, rr = nblocks & 7, xcd = b & 7, idx = b >> 3;
-  const int wid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + idx;
-  const int tile = wid % tiles;
-  const int row = wid / tiles;  // n * H + y
-  const int y = row % H;
-  const int n = row / H;
-  const int x0 = tile * kXT;
+  // work range of this workgroup's XCD group (blocks b and b+8 share an XCD)
+  const int grp = blockIdx.x & 7;
+  const int gi = blockIdx.x >> 3;
+  const int gsz = gridDim.x >> 3;
+  const int q = nwork >> 3, rr = nwork & 7;
+  const int wbeg = grp < rr ? grp * (q + 1) : rr * (q + 1) + (grp - rr) * q;
+  const int wend = wbeg + q + (grp < rr ? 1 : 0);
+  int w = wbeg + gi;
+  if (w >= wend) return;  // whole workgroup leaves together
 
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
   const int lane = tid & 63;
   const int fr = lane & 15;  // fragment row / column
   const int fk = lane >> 4;  // fragment k-chunk (8 channels)
+  const float fdiv = (float)divisor;
 
-  const T* Lrow = L + n * ls.n + (int64_t)y * ls.h;
-  const T* Rrow = R + n * rs.n + (int64_t)y * rs.h;
+  float rv[NR][8];  // in-flight right-window chunk (8 channels of one pixel per item)
+  float lv[8];      // in-flight left-tile chunk
 
-  for (int dp = 0; dp < D; dp += DMAX) {
-    const int Dp = min(DMAX, D - dp);
-    const int Tn = 1 + (Dp - 1 + 15) / 16;  // band blocks per x-block
-    const int RWIN = kXT + 16 * (Tn - 1);
-    const int js = x0 - dp - 16 * (Tn - 1);  // right column held in window row 0
-    unsigned char* Rt = smem;                           // P planes x RWIN rows
-    unsigned char* Lt = smem + P * RWIN * kRowBytes;    // P planes x 64 rows
-
-    f32x4 acc[TMAX];
+  auto issue = [&](const BandWork& k, int c0) {
+    const T* Rrow = R + k.n * rs.n + (int64_t)k.y * rs.h;
+    const T* Lrow = L + k.n * ls.n + (int64_t)k.y * ls.h;
 #pragma unroll
-    for (int t = 0; t < TMAX; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int it = 0; it < NR; ++it) {
+      const int e = tid + it * kThreads;
+      if (e < k.rwin * 4) {  // wave-uniform (rwin*4 is a multiple of 64)
+        const int ch = e / k.rwin;
+        const int r = e - ch * k.rwin;
+        load8(Rrow, rs.c, c0 + ch * 8, C, k.js + r, W, rv[it]);
+      }
+    }
+    load8(Lrow, ls.c, c0 + (tid >> 6) * 8, C, k.x0 + (tid & 63), W, lv);
+  };
 
-    for (int c0 = 0; c0 < C; c0 += kKC) {
-      __syncthreads();  // previous step's fragment reads (and the out tile) are done
-      // ---- stage the right window: thread -> (pixel row, 8-channel chunk), rows fastest
-      for (int e = tid; e < RWIN * 4; e += kThreads) {
-        const int ch = e / RWIN;
-        const int r = e - ch * RWIN;
-        const int j = js + r;
-        float v[8];
-        load8(Rrow, rs.c, c0 + ch * 8, C, j, W, v);
+  auto stage = [&](const BandWork& k) {
+    unsigned char* Rt = smem;
+    unsigned char* Lt = smem + P * k.rwin * kRowBytes;
+#pragma unroll
+    for (int it = 0; it < NR; ++it) {
+      const int e = tid + it * kThreads;
+      if (e < k.rwin * 4) {
+        const int ch = e / k.rwin;
+        const int r = e - ch * k.rwin;
         uint4 pk[P];
-        split8<P>(v, pk);
+        split8<P>(rv[it], pk);
 #pragma unroll
         for (int p = 0; p < P; ++p)
-          *reinterpret_cast<uint4*>(Rt + p * RWIN * kRowBytes + swz(r, ch)) = pk[p];
+          *reinterpret_cast<uint4*>(Rt + p * k.rwin * kRowBytes + swz(r, ch)) = pk[p];
       }
-      // ---- stage the left tile (64 pixel rows x 4 chunks = one element per thread)
-      {
-        const int ch = tid >> 6;
-        const int r = tid & 63;
-        const int x = x0 + r;
-        float v[8];
-        load8(Lrow, ls.c, c0 + ch * 8, C, x, W, v);
-        uint4 pk[P];
-        split8<P>(v, pk);
+    }
+    uint4 pk[P];
+    split8<P>(lv, pk);
 #pragma unroll
-        for (int p = 0; p < P; ++p)
-          *reinterpret_cast<uint4*>(Lt + p * kXT * kRowBytes + swz(r, ch)) = pk[p];
-      }
-      __syncthreads();
+    for (int p = 0; p < P; ++p)
+      *reinterpret_cast<uint4*>(Lt + p * kXT * kRowBytes + swz(tid & 63, tid >> 6)) = pk[p];
+  };
 
-      // ---- band MMA: B = left x-block (cols x), A = right j-block (rows j)
+  f32x4 acc[TMAX];
+  BandWork cur = band_decode(w, tiles, npass, H, D, DMAX);
+  int c0 = 0;
+  issue(cur, 0);
+
+  while (true) {
+    __syncthreads();  // previous fragment reads / out-tile reads are done
+    stage(cur);
+    __syncthreads();
+
+    // prefetch the next (work, channel step) before this step's MFMAs and epilogue
+    const bool last_step = c0 + kKC >= C;
+    const int nw = last_step ? w + gsz : w;
+    const int nc0 = last_step ? 0 : c0 + kKC;
+    const bool has_next = nw < wend;
+    const BandWork nxt = last_step ? band_decode(has_next ? nw : w, tiles, npass, H, D, DMAX) : cur;
+    if (has_next) issue(nxt, nc0);
+
+    if (c0 == 0) {
+#pragma unroll
+      for (int t = 0; t < TMAX; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+
+    // ---- band MMA: B = left x-block (cols x), A = right j-block (rows j)
+    {
+      const unsigned char* Rt = smem;
+      const unsigned char* Lt = smem + P * cur.rwin * kRowBytes;
       bf16x8 bq[P];
 #pragma unroll
       for (int p = 0; p < P; ++p)
         bq[p] = *reinterpret_cast<const bf16x8*>(Lt + p * kXT * kRowBytes + swz(16 * wave + fr, fk));
 #pragma unroll
       for (int t = 0; t < TMAX; ++t) {
-        if (t < Tn) {
+        if (t < cur.Tn) {
           bf16x8 aq[P];
 #pragma unroll
           for (int p = 0; p < P; ++p)
-            aq[p] = *reinterpret_cast<const bf16x8*>(Rt + p * RWIN * kRowBytes +
+            aq[p] = *reinterpret_cast<const bf16x8*>(Rt + p * cur.rwin * kRowBytes +
                                                      swz(16 * (wave + t) + fr, fk));
           if (P == 3) {
             acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[2], bq[0], acc[t], 0, 0, 0);
@@ -186,66 +260,77 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_mfma(
       }
     }
 
-    // ---- epilogue: shear S[j][x] -> out[d = x - j][x] through an LDS [Dp][64] fp32 tile
-    __syncthreads();
-    float* ot = reinterpret_cast<float*>(smem);
-    const int xl = 16 * wave + fr;  // this lane's pixel within the tile
-    const float fdiv = (float)divisor;
+    if (last_step) {
+      // ---- epilogue: shear S[j][x] -> out[d = x - j][x] through an LDS [Dp][64] fp32 tile
+      __syncthreads();
+      float* ot = reinterpret_cast<float*>(smem);
+      const int xl = 16 * wave + fr;
 #pragma unroll
-    for (int t = 0; t < TMAX; ++t) {
-      if (t < Tn) {
+      for (int t = 0; t < TMAX; ++t) {
+        if (t < cur.Tn) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          // window row of this accumulator element and its local disparity
-          const int wr = 16 * (wave + t) + 4 * fk + r;
-          const int dl = xl + 16 * (Tn - 1) - wr;
-          if (dl >= 0 && dl < Dp) {
-            const int j = js + wr;
-            float v = j >= 0 ? acc[t][r] : 0.f;  // x < d: exact zero, like torch.zeros
-            if (divisor >= 0 && j >= 0) v = v / fdiv;
-            ot[dl * kXT + xl] = v;
+          for (int r = 0; r < 4; ++r) {
+            const int wr = 16 * (wave + t) + 4 * fk + r;  // window row of this element
+            const int dl = xl + 16 * (cur.Tn - 1) - wr;   // its local disparity
+            if (dl >= 0 && dl < cur.Dp) {
+              const bool inside = cur.js + wr >= 0;  // j < 0 <=> x < d: exact zero
+              float v = inside ? acc[t][r] : 0.f;
+              if (divisor >= 0 && inside) v = v / fdiv;
+              ot[dl * kXT + xl] = v;
+            }
           }
         }
       }
-    }
-    __syncthreads();
-    const int c4 = tid & 15;
-    const int x = x0 + 4 * c4;
-    const bool fullrow = (x0 + kXT <= W) && ((W & 3) == 0);
-    for (int dl = tid >> 4; dl < Dp; dl += kThreads / 16) {
-      const float4 v = *reinterpret_cast<const float4*>(ot + dl * kXT + 4 * c4);
-      T* o = out + (((size_t)n * D + dp + dl) * H + y) * (size_t)W + x;
-      if (fullrow) {
-        if (sizeof(T) == 4) {
-          *reinterpret_cast<float4*>(o) = v;
-        } else {
-          union {
-            T e[4];
-            uint2 u;
-          } pk;
-          pk.e[0] = from_f<T>(v.x);
-          pk.e[1] = from_f<T>(v.y);
-          pk.e[2] = from_f<T>(v.z);
-          pk.e[3] = from_f<T>(v.w);
-          *reinterpret_cast<uint2*>(o) = pk.u;
+      __syncthreads();
+      const int c4 = tid & 15;
+      const int x = cur.x0 + 4 * c4;
+      const bool fullrow = (cur.x0 + kXT <= W) && ((W & 3) == 0);
+      if (fullrow) {  // 16-B aligned row segments: one wide store per lane per row
+        for (int dl = tid >> 4; dl < cur.Dp; dl += kThreads / 16) {
+          const float4 v = *reinterpret_cast<const float4*>(ot + dl * kXT + 4 * c4);
+          T* o = out + (((size_t)cur.n * D + cur.dp + dl) * H + cur.y) * (size_t)W + x;
+          store4(o, v);
         }
       } else {
-        const float vv[4] = {v.x, v.y, v.z, v.w};
+        for (int dl = tid >> 4; dl < cur.Dp; dl += kThreads / 16) {
+          const float4 v = *reinterpret_cast<const float4*>(ot + dl * kXT + 4 * c4);
+          T* o = out + (((size_t)cur.n * D + cur.dp + dl) * H + cur.y) * (size_t)W + x;
+          const float vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (x + k < W) o[k] = from_f<T>(vv[k]);
+          for (int k = 0; k < 4; ++k)
+            if (x + k < W) o[k] = from_f<T>(vv[k]);
+        }
       }
     }
+    if (!has_next) break;
+    w = nw;
+    c0 = nc0;
+    cur = nxt;
   }
+}
+
+int device_cus() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cached[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
 }
 
 template <typename T, int P, int TMAX>
 int launch_band(const void* l, const void* r, void* o, int64_t N, int64_t C, int64_t H, int64_t W,
                 int64_t D, Strides4 ls, Strides4 rs, int divisor, hipStream_t st) {
+  constexpr int DMAX = 16 * (TMAX - 1);
   const int tiles = (int)ceil_div(W, kXT);
-  const int64_t nb = (int64_t)tiles * H * N;
-  if (nb > INT32_MAX) return fail(SM_EINVAL, "inner product: grid too large");
-  const int Dp = (int)std::min<int64_t>(D, 16 * (TMAX - 1));
+  const int npass = (int)ceil_div(D, DMAX);
+  const int64_t nwork = (int64_t)tiles * H * N * npass;
+  if (nwork > INT32_MAX) return fail(SM_EINVAL, "inner product: too much work for one launch");
+  const int Dp = (int)std::min<int64_t>(D, DMAX);
   const int Tn = 1 + (Dp - 1 + 15) / 16;
   const int rwin = kXT + 16 * (Tn - 1);
   const size_t in_bytes = (size_t)P * (rwin + kXT) * kRowBytes;
@@ -255,11 +340,15 @@ int launch_band(const void* l, const void* r, void* o, int64_t N, int64_t C, int
   if (shm > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    if (e != hipSuccess) return fail(SM_ELAUNCH, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
+    if (e != hipSuccess)
+      return fail(SM_ELAUNCH, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
   }
-  hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(kThreads), shm, st, static_cast<const T*>(l),
+  // persistent grid: two workgroups per CU (LDS- and register-limited), a multiple of 8
+  int64_t nwg = std::min<int64_t>(nwork, 2 * (int64_t)device_cus());
+  nwg = std::max<int64_t>(8, (nwg + 7) / 8 * 8);
+  hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(kThreads), shm, st, static_cast<const T*>(l),
                      static_cast<const T*>(r), static_cast<T*>(o), (int)C, (int)H, (int)W, (int)D,
-                     ls, rs, divisor, tiles, (int)nb);
+                     ls, rs, divisor, tiles, npass, (int)nwork);
   return check_launch("ip_band_mfma");
 }
 

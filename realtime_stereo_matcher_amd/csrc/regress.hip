@@ -5,10 +5,10 @@
 //   presoftmax   disp = sum_d d * v              model/mobile_stereo_net_v4.py:10-14
 //   hard argext  first index of min/max over D   build-defined
 //
-// One lane owns one pixel; the wave sweeps 64 (x4 with float4 loads) consecutive pixels of a
-// row, so every load of a disparity plane is a coalesced 256 B / 1 KiB wave access.  The
-// softmax is a single streaming pass (online max with a rescale per 8-plane chunk) with
-// fp64 accumulators for sum(e) and sum(d*e): the result is within a few fp32 ulp of the
+// One lane owns one pixel (four with float4 loads) of a 64-lane row segment, so every load of
+// a disparity plane is a coalesced 256 B / 1 KiB wave access; the four waves of a block split
+// D.  The softmax is a single streaming pass (online max with a rescale per 8-plane chunk)
+// with fp64 accumulators for sum(e) and sum(d*e): the result is within a few fp32 ulp of the
 // exact value, i.e. the parity error budget is torch's own fp32 noise.
 #include "common.h"
 
@@ -24,16 +24,29 @@ struct VolView {
   int64_t n, d, h;  // element strides; W stride is 1
 };
 
+// Block = 4 waves over the SAME 64*PX pixels of a row; wave w owns the disparity quarter
+// [w*Dq, (w+1)*Dq).  Each lane keeps an online softmax (running max m, fp64 sums s = sum e,
+// t = sum d*e) per pixel; the four partial states are merged through LDS by wave 0.  Splitting
+// D across waves gives 4x the loads in flight of a one-wave-per-pixel sweep.
 template <typename T, int PX, bool PRESOFT>
 __global__ __launch_bounds__(kThreads) void softargmin_kernel(const T* __restrict__ vol,
                                                               T* __restrict__ out, int D, int H,
                                                               int W, VolView vs) {
+  __shared__ float sm_m[4][PX][64];
+  __shared__ double sm_s[4][PX][64];
+  __shared__ double sm_t[4][PX][64];
+  __shared__ int sm_nan[4][PX][64];
   const int y = blockIdx.y;
   const int n = blockIdx.z;
-  const int x0 = (blockIdx.x * kThreads + threadIdx.x) * PX;
-  if (x0 >= W) return;
-  const T* base = vol + n * vs.n + (int64_t)y * vs.h + x0;
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int x0 = (blockIdx.x * 64 + lane) * PX;
+  const bool any = x0 < W;
   const bool full = (x0 + PX) <= W;
+  const int Dq = (D + 3) >> 2;
+  const int dbeg = min(D, wave * Dq);
+  const int dend = min(D, dbeg + Dq);
+  const T* base = vol + n * vs.n + (int64_t)y * vs.h + (any ? x0 : 0);
 
   float m[PX];
   double s[PX], t[PX];
@@ -45,112 +58,180 @@ __global__ __launch_bounds__(kThreads) void softargmin_kernel(const T* __restric
     s[p] = 0.0;
     t[p] = 0.0;
   }
-  for (int d0 = 0; d0 < D; d0 += kChunk) {
-    const int nd = min(kChunk, D - d0);
-    float v[kChunk][PX];
+  if (any) {
+    for (int d0 = dbeg; d0 < dend; d0 += kChunk) {
+      const int nd = min(kChunk, dend - d0);
+      float v[kChunk][PX];
 #pragma unroll
-    for (int k = 0; k < kChunk; ++k) {
-      if (k < nd) {
-        const T* q = base + (int64_t)(d0 + k) * vs.d;
-        if (PX == 4 && full && sizeof(T) == 4) {
-          const float4 f = *reinterpret_cast<const float4*>(q);
+      for (int k = 0; k < kChunk; ++k) {
+        const T* qp = base + (int64_t)min(d0 + k, dend - 1) * vs.d;  // clamped: loads stay unconditional
+        if (PX == 4 && sizeof(T) == 4) {
+          float4 f;
+          if (full) {
+            f = *reinterpret_cast<const float4*>(qp);
+          } else {
+            f.x = to_f(qp[0]);
+            f.y = (x0 + 1 < W) ? to_f(qp[1]) : 0.f;
+            f.z = (x0 + 2 < W) ? to_f(qp[2]) : 0.f;
+            f.w = (x0 + 3 < W) ? to_f(qp[3]) : 0.f;
+          }
           v[k][0] = f.x;
           v[k][1 % PX] = f.y;
           v[k][2 % PX] = f.z;
           v[k][3 % PX] = f.w;
         } else {
 #pragma unroll
-          for (int p = 0; p < PX; ++p) v[k][p] = (x0 + p < W) ? to_f(q[p]) : 0.f;
+          for (int p = 0; p < PX; ++p) v[k][p] = (x0 + p < W) ? to_f(qp[p]) : 0.f;
         }
+        if (k >= nd) {
+#pragma unroll
+          for (int p = 0; p < PX; ++p) v[k][p] = -INFINITY;
+        }
+      }
+      if (PRESOFT) {
+#pragma unroll
+        for (int k = 0; k < kChunk; ++k)
+          if (k < nd)
+#pragma unroll
+            for (int p = 0; p < PX; ++p) t[p] += (double)(d0 + k) * (double)v[k][p];
       } else {
 #pragma unroll
-        for (int p = 0; p < PX; ++p) v[k][p] = -INFINITY;
-      }
-    }
-    if (PRESOFT) {
+        for (int p = 0; p < PX; ++p) {
+          float cm = v[0][p];
+          bool nan = v[0][p] != v[0][p];
 #pragma unroll
-      for (int k = 0; k < kChunk; ++k)
-        if (k < nd)
+          for (int k = 1; k < kChunk; ++k) {
+            cm = fmaxf(cm, v[k][p]);
+            nan |= v[k][p] != v[k][p];
+          }
+          has_nan[p] |= nan;
+          if (cm == -INFINITY) continue;  // nothing finite yet in this chunk
+          if (cm > m[p]) {                 // new running max: rescale once per chunk
+            const double f = (m[p] == -INFINITY) ? 0.0 : (double)expf(m[p] - cm);
+            s[p] *= f;
+            t[p] *= f;
+            m[p] = cm;
+          }
 #pragma unroll
-          for (int p = 0; p < PX; ++p) t[p] += (double)(d0 + k) * (double)v[k][p];
-    } else {
-#pragma unroll
-      for (int p = 0; p < PX; ++p) {
-        float cm = v[0][p];
-        bool nan = v[0][p] != v[0][p];
-#pragma unroll
-        for (int k = 1; k < kChunk; ++k) {
-          cm = fmaxf(cm, v[k][p]);
-          nan |= v[k][p] != v[k][p];
-        }
-        has_nan[p] |= nan;
-        if (cm == -INFINITY) continue;  // nothing finite yet in this chunk (or column)
-        if (cm > m[p]) {  // new running max: rescale the accumulators once per chunk
-          const double f = (m[p] == -INFINITY) ? 0.0 : (double)expf(m[p] - cm);
-          s[p] *= f;
-          t[p] *= f;
-          m[p] = cm;
-        }
-#pragma unroll
-        for (int k = 0; k < kChunk; ++k) {
-          if (k < nd) {
-            const float e = expf(v[k][p] - m[p]);
-            s[p] += (double)e;
-            t[p] += (double)(d0 + k) * (double)e;
+          for (int k = 0; k < kChunk; ++k) {
+            if (k < nd) {
+              const float e = expf(v[k][p] - m[p]);
+              s[p] += (double)e;
+              t[p] += (double)(d0 + k) * (double)e;
+            }
           }
         }
       }
     }
   }
+  // ---- merge the four disparity quarters
+#pragma unroll
+  for (int p = 0; p < PX; ++p) {
+    sm_m[wave][p][lane] = m[p];
+    sm_s[wave][p][lane] = s[p];
+    sm_t[wave][p][lane] = t[p];
+    sm_nan[wave][p][lane] = has_nan[p];
+  }
+  __syncthreads();
+  if (wave != 0 || !any) return;
   T* o = out + ((int64_t)n * H + y) * W + x0;
 #pragma unroll
   for (int p = 0; p < PX; ++p) {
-    if (x0 + p < W) {
-      float r;
-      if (PRESOFT) {
-        r = (float)t[p];
-      } else if (D == 0) {
-        r = 0.f;  // empty softmax axis: the weighted sum is empty -> 0
-      } else {
-        // NaN anywhere in the column, or an all -inf / any +inf column, gives NaN as in torch
-        r = (has_nan[p] || m[p] == INFINITY || m[p] == -INFINITY) ? NAN : (float)(t[p] / s[p]);
+    if (x0 + p >= W) continue;
+    float r;
+    if (PRESOFT) {
+      double tt = 0.0;
+      for (int w = 0; w < 4; ++w) tt += sm_t[w][p][lane];
+      r = (float)tt;
+    } else if (D == 0) {
+      r = 0.f;  // empty softmax axis: the weighted sum is empty -> 0
+    } else {
+      float M = -INFINITY;
+      bool nan = false;
+      for (int w = 0; w < 4; ++w) {
+        M = fmaxf(M, sm_m[w][p][lane]);
+        nan |= sm_nan[w][p][lane] != 0;
       }
-      o[p] = from_f<T>(r);
+      double S = 0.0, Tt = 0.0;
+      if (M != -INFINITY && M != INFINITY) {
+        for (int w = 0; w < 4; ++w) {
+          const float mw = sm_m[w][p][lane];
+          if (mw == -INFINITY) continue;
+          const double f = (double)expf(mw - M);
+          S += sm_s[w][p][lane] * f;
+          Tt += sm_t[w][p][lane] * f;
+        }
+      }
+      // NaN anywhere in the column, or an all -inf / any +inf column, gives NaN as in torch
+      r = (nan || M == INFINITY || M == -INFINITY) ? NAN : (float)(Tt / S);
     }
+    o[p] = from_f<T>(r);
   }
 }
 
+// Hard argmin/argmax with the same 4-wave disparity split; the quarters are merged in
+// disparity order with the same strict comparison, so the FIRST extreme index wins.
 template <typename T, bool MAXMODE>
 __global__ __launch_bounds__(kThreads) void argext_kernel(const T* __restrict__ vol,
                                                           int64_t* __restrict__ out, int D, int H,
                                                           int W, VolView vs) {
+  __shared__ float sm_b[4][64];
+  __shared__ int sm_i[4][64];
   const int y = blockIdx.y;
   const int n = blockIdx.z;
-  const int x = blockIdx.x * kThreads + threadIdx.x;
-  if (x >= W) return;
-  const T* base = vol + n * vs.n + (int64_t)y * vs.h + x;
-  float best = to_f(base[0]);
-  int idx = 0;
-  bool isnan_best = best != best;
-  for (int d0 = 1; d0 < D; d0 += kChunk) {
-    float v[kChunk];
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int x = blockIdx.x * 64 + lane;
+  const bool ok = x < W;
+  const int Dq = (D + 3) >> 2;
+  const int dbeg = min(D, wave * Dq);
+  const int dend = min(D, dbeg + Dq);
+  const T* base = vol + n * vs.n + (int64_t)y * vs.h + (ok ? x : 0);
+  float best = MAXMODE ? -INFINITY : INFINITY;
+  int idx = -1;  // -1: this quarter is empty
+  bool isnan_best = false;
+  if (ok) {
+    for (int d0 = dbeg; d0 < dend; d0 += kChunk) {
+      float v[kChunk];
 #pragma unroll
-    for (int k = 0; k < kChunk; ++k)
-      v[k] = (d0 + k < D) ? to_f(base[(int64_t)(d0 + k) * vs.d]) : (MAXMODE ? -INFINITY : INFINITY);
+      for (int k = 0; k < kChunk; ++k) v[k] = to_f(base[(int64_t)min(d0 + k, dend - 1) * vs.d]);
 #pragma unroll
-    for (int k = 0; k < kChunk; ++k) {
-      if (d0 + k < D && !isnan_best) {
-        const bool vnan = v[k] != v[k];
-        const bool better = MAXMODE ? (v[k] > best) : (v[k] < best);  // strict: first index wins
-        if (vnan || better) {
-          best = v[k];
-          idx = d0 + k;
-          isnan_best = vnan;
+      for (int k = 0; k < kChunk; ++k) {
+        if (d0 + k < dend && !isnan_best) {
+          const bool vnan = v[k] != v[k];
+          const bool better = idx < 0 || (MAXMODE ? (v[k] > best) : (v[k] < best));
+          if (vnan || better) {
+            best = v[k];
+            idx = d0 + k;
+            isnan_best = vnan;
+          }
         }
       }
     }
   }
-  out[((int64_t)n * H + y) * W + x] = idx;
+  sm_b[wave][lane] = best;
+  sm_i[wave][lane] = idx;
+  __syncthreads();
+  if (wave != 0 || !ok) return;
+  float B = 0.f;
+  int I = -1;
+  for (int w = 0; w < 4; ++w) {
+    const int iw = sm_i[w][lane];
+    if (iw < 0) continue;
+    const float bw = sm_b[w][lane];
+    if (I < 0) {
+      B = bw;
+      I = iw;
+      continue;
+    }
+    if (B != B) break;  // a NaN already won
+    const bool better = (bw != bw) || (MAXMODE ? (bw > B) : (bw < B));
+    if (better) {
+      B = bw;
+      I = iw;
+    }
+  }
+  out[((int64_t)n * H + y) * W + x] = I < 0 ? 0 : I;
 }
 
 int check_vol(const void* volume, const void* out, int dtype, int64_t N, int64_t D, int64_t H,
@@ -191,7 +272,7 @@ int softargmin_entry(const void* volume, void* out, int dtype, int64_t N, int64_
     const T* v = static_cast<const T*>(volume);
     T* o = static_cast<T*>(out);
     if (v4) {
-      dim3 grid((unsigned)ceil_div(W, kThreads * 4), (unsigned)H, (unsigned)N);
+      dim3 grid((unsigned)ceil_div(W, 64 * 4), (unsigned)H, (unsigned)N);
       if (presoft)
         hipLaunchKernelGGL((softargmin_kernel<T, 4, true>), grid, dim3(kThreads), 0, st, v, o,
                            (int)D, (int)H, (int)W, vs);
@@ -199,7 +280,7 @@ int softargmin_entry(const void* volume, void* out, int dtype, int64_t N, int64_
         hipLaunchKernelGGL((softargmin_kernel<T, 4, false>), grid, dim3(kThreads), 0, st, v, o,
                            (int)D, (int)H, (int)W, vs);
     } else {
-      dim3 grid((unsigned)ceil_div(W, kThreads), (unsigned)H, (unsigned)N);
+      dim3 grid((unsigned)ceil_div(W, 64), (unsigned)H, (unsigned)N);
       if (presoft)
         hipLaunchKernelGGL((softargmin_kernel<T, 1, true>), grid, dim3(kThreads), 0, st, v, o,
                            (int)D, (int)H, (int)W, vs);
@@ -220,7 +301,7 @@ int argext_entry(const void* volume, int64_t* out, int dtype, int64_t N, int64_t
   if (N * H * W == 0) return SM_OK;
   if (D <= 0) return fail(SM_EINVAL, "argext over an empty D axis");
   hipStream_t st = as_stream(stream);
-  dim3 grid((unsigned)ceil_div(W, kThreads), (unsigned)H, (unsigned)N);
+  dim3 grid((unsigned)ceil_div(W, 64), (unsigned)H, (unsigned)N);
   SM_DISPATCH_DTYPE(dtype, T, {
     const T* v = static_cast<const T*>(volume);
     if (mode == SM_ARGMAX)
