@@ -26,6 +26,8 @@
 // the overlapping right windows).
 #include "common.h"
 
+#include <cstdlib>
+
 namespace smcv {
 namespace {
 
@@ -142,7 +144,7 @@ __device__ __forceinline__ BandWork band_decode(int w, int tiles, int npass, int
 template <typename T, int P, int TMAX>
 __global__ __launch_bounds__(kThreads, 2) void ip_band_mfma(
     const T* __restrict__ L, const T* __restrict__ R, T* __restrict__ out, int C, int H, int W,
-    int D, Strides4 ls, Strides4 rs, int divisor, int tiles, int npass, int nwork) {
+    int D, Strides4 ls, Strides4 rs, int divisor, int tiles, int npass, int nwork, int ablate) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int DMAX = 16 * (TMAX - 1);
   constexpr int NR = (3 + TMAX) / 4;  // window staging items per thread = RWIN*4/256 at Tn=TMAX
@@ -221,7 +223,7 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_mfma(
     const int nc0 = last_step ? 0 : c0 + kKC;
     const bool has_next = nw < wend;
     const BandWork nxt = last_step ? band_decode(has_next ? nw : w, tiles, npass, H, D, DMAX) : cur;
-    if (has_next) issue(nxt, nc0);
+    if (has_next && !(ablate & 2)) issue(nxt, nc0);
 
     if (c0 == 0) {
 #pragma unroll
@@ -238,7 +240,7 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_mfma(
         bq[p] = *reinterpret_cast<const bf16x8*>(Lt + p * kXT * kRowBytes + swz(16 * wave + fr, fk));
 #pragma unroll
       for (int t = 0; t < TMAX; ++t) {
-        if (t < cur.Tn) {
+        if (t < cur.Tn && !(ablate & 1)) {
           bf16x8 aq[P];
 #pragma unroll
           for (int p = 0; p < P; ++p)
@@ -285,7 +287,9 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_mfma(
       const int c4 = tid & 15;
       const int x = cur.x0 + 4 * c4;
       const bool fullrow = (cur.x0 + kXT <= W) && ((W & 3) == 0);
-      if (fullrow) {  // 16-B aligned row segments: one wide store per lane per row
+      if (ablate & 4) {
+        // diagnostic build path: no output stream
+      } else if (fullrow) {  // 16-B aligned row segments: one wide store per lane per row
         for (int dl = tid >> 4; dl < cur.Dp; dl += kThreads / 16) {
           const float4 v = *reinterpret_cast<const float4*>(ot + dl * kXT + 4 * c4);
           T* o = out + (((size_t)cur.n * D + cur.dp + dl) * H + cur.y) * (size_t)W + x;
@@ -307,6 +311,13 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_mfma(
     c0 = nc0;
     cur = nxt;
   }
+}
+
+// Diagnostic ablation bits (STEREOCV_ABLATE, timing studies only; outputs become garbage):
+// 1 = skip MFMAs, 2 = skip the global loads of the pipelined steps, 4 = skip output stores.
+int ablate_bits() {
+  const char* e = getenv("STEREOCV_ABLATE");
+  return e ? atoi(e) : 0;
 }
 
 int device_cus() {
@@ -348,7 +359,7 @@ int launch_band(const void* l, const void* r, void* o, int64_t N, int64_t C, int
   nwg = std::max<int64_t>(8, (nwg + 7) / 8 * 8);
   hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(kThreads), shm, st, static_cast<const T*>(l),
                      static_cast<const T*>(r), static_cast<T*>(o), (int)C, (int)H, (int)W, (int)D,
-                     ls, rs, divisor, tiles, npass, (int)nwork);
+                     ls, rs, divisor, tiles, npass, (int)nwork, ablate_bits());
   return check_launch("ip_band_mfma");
 }
 
