@@ -5,8 +5,8 @@
 //   out[n, d, y, x] = sum_c L[n,c,y,x] * R[n,c,y,x-d]   (x >= d),   0 (x < d)
 //
 // Per image row the volume is a BAND of the C-contraction S[j][x] = sum_c R[c][j] L[c][x]
-// (d = x - j in [0, D)).  One workgroup owns a row segment of 64 left pixels; each of its four
-// waves owns a 16-pixel x-block and accumulates the T = 1 + ceil((D-1)/16) 16x16 S-blocks of its
+// (d = x - j in [0, D)).  One workgroup (8 waves) owns a row segment of 128 left pixels; wave w
+// owns the 16-pixel x-block w and accumulates the T = 1 + ceil((D-1)/16) 16x16 S-blocks of its
 // band (8 % over-compute at D = 192) with v_mfma_f32_16x16x32_bf16, K = 32 channels per step.
 //
 // fp32 features are split EXACTLY into three bf16 planes (x = h + m + l, 8+8+8 significand
@@ -16,14 +16,17 @@
 // fp16 features need two planes (11 bits) and 4 products (exact products); bf16 needs one.
 // The matrix cores run at 16x the fp32 rate, so even 6 products leave the kernel HBM-bound.
 //
-// Data path per 32-channel step: the right WINDOW R[j0 .. j0+64+16(T-1)) and the left tile are
-// loaded (coalesced along the row), split, and written to LDS pixel-major ([pixel][32 ch], 64 B
-// per row and plane) with an XOR chunk swizzle that makes every ds_read_b128 fragment read
-// bank-conflict free; the window is re-used by all T blocks of all four waves (the disparity
-// sweep never re-reads HBM).  Epilogue: the accumulators are sheared (d = x - j) into an LDS
-// [D][64] fp32 tile and streamed out as 256-B row segments (out rows are x-contiguous).
-// Workgroups are remapped so that the x-tiles of one image row run on one XCD (shared L2 for
-// the overlapping right windows).
+// Staging per 32-channel step: the right WINDOW R[j0 .. j0+128+16(T-1)) and the left tile are
+// loaded as (8 channels x 4 pixels) items -- eight 16-B loads per lane, coalesced along the
+// row -- split, and written to LDS pixel-major ([pixel][32 ch], 64 B per row and plane) under an
+// XOR chunk swizzle that makes every ds_read_b128 fragment read bank-conflict free (staging
+// writes are at most 2-way).  The window is re-used by all T blocks of all eight waves, so the
+// disparity sweep never re-reads HBM.  The workgroup is persistent: the loads of the next step
+// (or the next row segment) are issued into registers before the current step's MFMAs and
+// epilogue, hiding HBM latency.  Epilogue: the accumulators are sheared (d = x - j) into an LDS
+// [D][128] fp32 tile and streamed out as 512-B row segments (out rows are x-contiguous).
+// Workgroups b and b+8 share an XCD; each XCD group walks its own contiguous range of row
+// segments, so concurrently running segments of one row share that XCD's L2.
 #include "common.h"
 
 #include <cstdlib>
@@ -34,45 +37,24 @@ namespace {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kThreads = 256;
-constexpr int kXT = 64;        // left pixels per workgroup (4 waves x 16)
-constexpr int kKC = 32;        // channels per MFMA k-step
-constexpr int kRowBytes = 64;  // one LDS pixel row of one plane: 32 bf16
+constexpr int kWaves = 8;
+constexpr int kThreads = 64 * kWaves;
+constexpr int kXT = 16 * kWaves;  // left pixels per row segment
+constexpr int kKC = 32;           // channels per MFMA k-step
+constexpr int kRowBytes = 64;     // one LDS pixel row of one plane: 32 bf16
 
-// byte offset of (pixel row r, 16-B channel chunk ch) inside one plane: conflict-free for the
-// 16x16x32 fragment read pattern (lane l -> row l&15, chunk l>>4) under the four ds_read_b128
-// lane groups of gfx950 (MI355X_MICROARCH.md §LDS).
-__device__ __forceinline__ int swz(int r, int ch) { return r * kRowBytes + 16 * (ch ^ ((r >> 2) & 2)); }
-
-// 8 consecutive channels [cb, cb+8) of pixel j of one feature row; zero outside the image or
-// past C.  Addresses are clamped and masked with selects (no branch around the loads, so the
-// eight loads stay in flight together).
-template <typename T>
-__device__ __forceinline__ void load8(const T* __restrict__ rowp, int64_t cstride, int cb, int C,
-                                      int j, int W, float (&v)[8]) {
-  const bool okj = (j >= 0) && (j < W);
-  const int jc = min(max(j, 0), W - 1);
-  if (C <= 0) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = 0.f;
-    return;
-  }
-  if (cb + 8 <= C) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = to_f(rowp[(int64_t)(cb + i) * cstride + jc]);
-  } else {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = to_f(rowp[(int64_t)min(cb + i, C - 1) * cstride + jc]);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = (cb + i < C) ? v[i] : 0.f;
-  }
-#pragma unroll
-  for (int i = 0; i < 8; ++i) v[i] = okj ? v[i] : 0.f;
+// byte offset of (pixel row r, 16-B channel chunk ch) inside one plane.  With the chunk XOR
+// f = {0,2,3,1}[(r>>2)&3] the 16x16x32 fragment read (lane l -> row l&15, chunk l>>4) is
+// conflict-free under all four gfx950 ds_read_b128 lane groups, and the staging writes
+// (8 contiguous lanes per LDS cycle) are at most 2-way (checked in scripts/check_swizzle.py).
+__device__ __forceinline__ int swz(int r, int ch) {
+  const int f = (0x78 >> (2 * ((r >> 2) & 3))) & 3;  // {0, 2, 3, 1}
+  return r * kRowBytes + 16 * (ch ^ f);
 }
 
+// Exact split of 8 floats into P bf16 planes (x = h + m + l); non-finite values stay whole in h.
 template <int P>
 __device__ __forceinline__ void split8(const float (&v)[8], uint4 (&q)[P]) {
-  // exact split x = h + m + l into bf16 planes (non-finite values keep everything in h)
   union U {
     __bf16 b[8];
     uint4 u;
@@ -84,8 +66,8 @@ __device__ __forceinline__ void split8(const float (&v)[8], uint4 (&q)[P]) {
     const __bf16 bh = (__bf16)x;
     h.b[i] = bh;
     if (P > 1) {
-      const bool fin = __builtin_isfinite(x);
-      const float r1 = fin ? x - (float)bh : 0.f;
+      float r1 = x - (float)bh;
+      r1 = __builtin_isfinite(x) ? r1 : 0.f;
       const __bf16 bm = (__bf16)r1;
       m.b[i] = bm;
       if (P > 2) l.b[i] = (__bf16)(r1 - (float)bm);
@@ -94,6 +76,25 @@ __device__ __forceinline__ void split8(const float (&v)[8], uint4 (&q)[P]) {
   q[0] = h.u;
   if (P > 1) q[1] = m.u;
   if (P > 2) q[2] = l.u;
+}
+
+template <typename T>
+__device__ __forceinline__ void load4(const T* p, float (&o)[4]) {
+  if constexpr (sizeof(T) == 4) {
+    const float4 f = *reinterpret_cast<const float4*>(p);
+    o[0] = f.x;
+    o[1] = f.y;
+    o[2] = f.z;
+    o[3] = f.w;
+  } else {
+    union {
+      uint2 u;
+      T e[4];
+    } q;
+    q.u = *reinterpret_cast<const uint2*>(p);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = to_f(q.e[i]);
+  }
 }
 
 // 4 consecutive outputs (16-B aligned for fp32, 8-B for 16-bit types) in one store.
@@ -114,13 +115,14 @@ __device__ __forceinline__ void store4(T* o, float4 v) {
   }
 }
 
-// One unit of work: a 64-pixel segment of one image row and one pass of at most DMAX
-// disparities.  Consecutive work ids are the x-tiles of one row (they share right columns).
+// One unit of work: a 128-pixel segment of one image row and one pass of at most DMAX
+// disparities.  Consecutive work ids are the segments of one row (they share right columns).
 struct BandWork {
   int n, y, x0, dp, Dp, Tn, rwin, js;
 };
 
-__device__ __forceinline__ BandWork band_decode(int w, int tiles, int npass, int H, int D, int dmax) {
+__device__ __forceinline__ BandWork band_decode(int w, int tiles, int npass, int H, int D,
+                                                int dmax) {
   BandWork k;
   const int pass = w % npass;
   const int rest = w / npass;
@@ -137,17 +139,28 @@ __device__ __forceinline__ BandWork band_decode(int w, int tiles, int npass, int
   return k;
 }
 
-// Persistent, software-pipelined band kernel.  Each workgroup walks a contiguous range of
-// work ids owned by its XCD group; the global loads of the NEXT (work, 32-channel step) are
-// issued into registers before the MFMAs and the epilogue of the current one, so HBM latency
-// hides behind compute and the output stream.
-template <typename T, int P, int TMAX>
-__global__ __launch_bounds__(kThreads, 2) void ip_band_mfma(
+template <typename T>
+struct StageItem {
+  const T* row;  // feature row (n, c = 0, y) of L or R
+  int64_t cstride;
+  int j0;     // first pixel of the 4-pixel group
+  int chunk;  // 8-channel chunk inside the 32-channel step
+  int lrow;   // first LDS pixel row
+  bool isR, active;
+};
+
+template <typename T, int P, int TMAX, bool VEC>
+__global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
     const T* __restrict__ L, const T* __restrict__ R, T* __restrict__ out, int C, int H, int W,
     int D, Strides4 ls, Strides4 rs, int divisor, int tiles, int npass, int nwork, int ablate) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int DMAX = 16 * (TMAX - 1);
-  constexpr int NR = (3 + TMAX) / 4;  // window staging items per thread = RWIN*4/256 at Tn=TMAX
+  constexpr int RWMAX = kXT + DMAX;           // window rows at Tn = TMAX
+  constexpr int PLANE_R = RWMAX * kRowBytes;  // compile-time plane strides
+  constexpr int PLANE_L = kXT * kRowBytes;
+  static_assert((RWMAX + kXT) <= kThreads * 4 / 4, "one staging item per thread");
+  unsigned char* const Rt = smem;
+  unsigned char* const Lt = smem + P * PLANE_R;
 
   // work range of this workgroup's XCD group (blocks b and b+8 share an XCD)
   const int grp = blockIdx.x & 7;
@@ -157,7 +170,7 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_mfma(
   const int wbeg = grp < rr ? grp * (q + 1) : rr * (q + 1) + (grp - rr) * q;
   const int wend = wbeg + q + (grp < rr ? 1 : 0);
   int w = wbeg + gi;
-  if (w >= wend) return;  // whole workgroup leaves together
+  if (w >= wend) return;  // the whole workgroup leaves together
 
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
@@ -166,64 +179,96 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_mfma(
   const int fk = lane >> 4;  // fragment k-chunk (8 channels)
   const float fdiv = (float)divisor;
 
-  float rv[NR][8];  // in-flight right-window chunk (8 channels of one pixel per item)
-  float lv[8];      // in-flight left-tile chunk
-
-  auto issue = [&](const BandWork& k, int c0) {
-    const T* Rrow = R + k.n * rs.n + (int64_t)k.y * rs.h;
-    const T* Lrow = L + k.n * ls.n + (int64_t)k.y * ls.h;
-#pragma unroll
-    for (int it = 0; it < NR; ++it) {
-      const int e = tid + it * kThreads;
-      if (e < k.rwin * 4) {  // wave-uniform (rwin*4 is a multiple of 64)
-        const int ch = e / k.rwin;
-        const int r = e - ch * k.rwin;
-        load8(Rrow, rs.c, c0 + ch * 8, C, k.js + r, W, rv[it]);
-      }
-    }
-    load8(Lrow, ls.c, c0 + (tid >> 6) * 8, C, k.x0 + (tid & 63), W, lv);
+  // ---- this thread's staging item: (8-channel chunk, 4-pixel group) of the window or tile
+  float v[8][4];  // in-flight item: 8 channels x 4 pixels
+  auto make_item = [&](const BandWork& k) {
+    StageItem<T> it;
+    const bool isR = tid < k.rwin;
+    const int i = isR ? tid : tid - k.rwin;
+    it.isR = isR;
+    it.active = tid < k.rwin + kXT;
+    it.chunk = i & 3;
+    it.lrow = 4 * (i >> 2);
+    it.j0 = (isR ? k.js : k.x0) + it.lrow;
+    it.row = isR ? R + k.n * rs.n + (int64_t)k.y * rs.h : L + k.n * ls.n + (int64_t)k.y * ls.h;
+    it.cstride = isR ? rs.c : ls.c;
+    return it;
   };
-
-  auto stage = [&](const BandWork& k) {
-    unsigned char* Rt = smem;
-    unsigned char* Lt = smem + P * k.rwin * kRowBytes;
+  auto issue = [&](const StageItem<T>& it, int c0) {
+    const int cb = c0 + 8 * it.chunk;
+    if (!it.active) return;
+    if (VEC) {
+      // W % 4 == 0 and j0 % 4 == 0: the 4-pixel group is entirely inside or outside the row
+      const bool okj = it.j0 >= 0 && it.j0 < W;
+      const int jc = okj ? it.j0 : 0;
 #pragma unroll
-    for (int it = 0; it < NR; ++it) {
-      const int e = tid + it * kThreads;
-      if (e < k.rwin * 4) {
-        const int ch = e / k.rwin;
-        const int r = e - ch * k.rwin;
-        uint4 pk[P];
-        split8<P>(rv[it], pk);
+      for (int k = 0; k < 8; ++k) {
+        const int c = min(cb + k, C - 1);
+        load4(it.row + (int64_t)c * it.cstride + jc, v[k]);
+      }
 #pragma unroll
-        for (int p = 0; p < P; ++p)
-          *reinterpret_cast<uint4*>(Rt + p * k.rwin * kRowBytes + swz(r, ch)) = pk[p];
+      for (int k = 0; k < 8; ++k) {
+        const bool ok = okj && (cb + k < C);
+#pragma unroll
+        for (int p = 0; p < 4; ++p) v[k][p] = ok ? v[k][p] : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int c = min(cb + k, C - 1);
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const int j = it.j0 + p;
+          const int jc = min(max(j, 0), W - 1);
+          const float x = to_f(it.row[(int64_t)c * it.cstride + jc]);
+          v[k][p] = (j >= 0 && j < W && cb + k < C) ? x : 0.f;
+        }
       }
     }
-    uint4 pk[P];
-    split8<P>(lv, pk);
+  };
+  auto stage = [&](const StageItem<T>& it) {
+    if (!it.active) return;
+    unsigned char* base = it.isR ? Rt : Lt;
+    const int pstride = it.isR ? PLANE_R : PLANE_L;
 #pragma unroll
-    for (int p = 0; p < P; ++p)
-      *reinterpret_cast<uint4*>(Lt + p * kXT * kRowBytes + swz(tid & 63, tid >> 6)) = pk[p];
+    for (int p = 0; p < 4; ++p) {
+      float col[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) col[k] = v[k][p];
+      uint4 pk[P];
+      split8<P>(col, pk);
+      const int off = swz(it.lrow + p, it.chunk);
+#pragma unroll
+      for (int pl = 0; pl < P; ++pl) *reinterpret_cast<uint4*>(base + pl * pstride + off) = pk[pl];
+    }
   };
 
   f32x4 acc[TMAX];
   BandWork cur = band_decode(w, tiles, npass, H, D, DMAX);
+  StageItem<T> item = make_item(cur);
   int c0 = 0;
-  issue(cur, 0);
+  if (C <= 0 || (ablate & 2)) {  // empty channel axis: zero sum (mean: 0/0 = NaN, as torch)
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int p = 0; p < 4; ++p) v[k][p] = 0.f;
+  } else {
+    issue(item, 0);
+  }
 
   while (true) {
     __syncthreads();  // previous fragment reads / out-tile reads are done
-    stage(cur);
+    stage(item);
     __syncthreads();
 
-    // prefetch the next (work, channel step) before this step's MFMAs and epilogue
+    // prefetch the next (segment, channel step) before this step's MFMAs and epilogue
     const bool last_step = c0 + kKC >= C;
     const int nw = last_step ? w + gsz : w;
     const int nc0 = last_step ? 0 : c0 + kKC;
     const bool has_next = nw < wend;
     const BandWork nxt = last_step ? band_decode(has_next ? nw : w, tiles, npass, H, D, DMAX) : cur;
-    if (has_next && !(ablate & 2)) issue(nxt, nc0);
+    const StageItem<T> nitem = last_step ? make_item(nxt) : item;
+    if (has_next && !(ablate & 2)) issue(nitem, nc0);
 
     if (c0 == 0) {
 #pragma unroll
@@ -231,21 +276,19 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_mfma(
     }
 
     // ---- band MMA: B = left x-block (cols x), A = right j-block (rows j)
-    {
-      const unsigned char* Rt = smem;
-      const unsigned char* Lt = smem + P * cur.rwin * kRowBytes;
+    if (!(ablate & 1)) {
       bf16x8 bq[P];
+      const int boff = swz(16 * wave + fr, fk);
 #pragma unroll
-      for (int p = 0; p < P; ++p)
-        bq[p] = *reinterpret_cast<const bf16x8*>(Lt + p * kXT * kRowBytes + swz(16 * wave + fr, fk));
+      for (int p = 0; p < P; ++p) bq[p] = *reinterpret_cast<const bf16x8*>(Lt + p * PLANE_L + boff);
+      const int aoff = swz(16 * wave + fr, fk);  // + 1024 * t (the swizzle is 16-row periodic)
 #pragma unroll
       for (int t = 0; t < TMAX; ++t) {
-        if (t < cur.Tn && !(ablate & 1)) {
+        if (t < cur.Tn) {
           bf16x8 aq[P];
 #pragma unroll
           for (int p = 0; p < P; ++p)
-            aq[p] = *reinterpret_cast<const bf16x8*>(Rt + p * cur.rwin * kRowBytes +
-                                                     swz(16 * (wave + t) + fr, fk));
+            aq[p] = *reinterpret_cast<const bf16x8*>(Rt + p * PLANE_R + aoff + 1024 * t);
           if (P == 3) {
             acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[2], bq[0], acc[t], 0, 0, 0);
             acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[1], bq[1], acc[t], 0, 0, 0);
@@ -263,43 +306,44 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_mfma(
     }
 
     if (last_step) {
-      // ---- epilogue: shear S[j][x] -> out[d = x - j][x] through an LDS [Dp][64] fp32 tile
+      // ---- epilogue: shear S[j][x] -> out[d = x - j][x] through an LDS [Dp][128] fp32 tile
       __syncthreads();
       float* ot = reinterpret_cast<float*>(smem);
       const int xl = 16 * wave + fr;
+      // local disparity of accumulator (t, r): dl = b0 - 16 t - r
+      const int b0 = fr - 4 * fk + 16 * (cur.Tn - 1);
+      const int j_b = cur.js + 16 * wave + 4 * fk;  // right column of (t = 0, r = 0)
 #pragma unroll
       for (int t = 0; t < TMAX; ++t) {
         if (t < cur.Tn) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int wr = 16 * (wave + t) + 4 * fk + r;  // window row of this element
-            const int dl = xl + 16 * (cur.Tn - 1) - wr;   // its local disparity
+            const int dl = b0 - 16 * t - r;
             if (dl >= 0 && dl < cur.Dp) {
-              const bool inside = cur.js + wr >= 0;  // j < 0 <=> x < d: exact zero
-              float v = inside ? acc[t][r] : 0.f;
-              if (divisor >= 0 && inside) v = v / fdiv;
-              ot[dl * kXT + xl] = v;
+              const bool inside = j_b + 16 * t + r >= 0;  // j < 0 <=> x < d: exact zero
+              float val = inside ? acc[t][r] : 0.f;
+              if (divisor >= 0) val = inside ? val / fdiv : 0.f;
+              ot[dl * kXT + xl] = val;
             }
           }
         }
       }
       __syncthreads();
-      const int c4 = tid & 15;
+      const int c4 = tid & 31;
       const int x = cur.x0 + 4 * c4;
       const bool fullrow = (cur.x0 + kXT <= W) && ((W & 3) == 0);
       if (ablate & 4) {
-        // diagnostic build path: no output stream
+        // diagnostic path: no output stream
       } else if (fullrow) {  // 16-B aligned row segments: one wide store per lane per row
-        for (int dl = tid >> 4; dl < cur.Dp; dl += kThreads / 16) {
-          const float4 v = *reinterpret_cast<const float4*>(ot + dl * kXT + 4 * c4);
-          T* o = out + (((size_t)cur.n * D + cur.dp + dl) * H + cur.y) * (size_t)W + x;
-          store4(o, v);
+        for (int dl = tid >> 5; dl < cur.Dp; dl += kThreads / 32) {
+          const float4 val = *reinterpret_cast<const float4*>(ot + dl * kXT + 4 * c4);
+          store4(out + (((size_t)cur.n * D + cur.dp + dl) * H + cur.y) * (size_t)W + x, val);
         }
       } else {
-        for (int dl = tid >> 4; dl < cur.Dp; dl += kThreads / 16) {
-          const float4 v = *reinterpret_cast<const float4*>(ot + dl * kXT + 4 * c4);
+        for (int dl = tid >> 5; dl < cur.Dp; dl += kThreads / 32) {
+          const float4 val = *reinterpret_cast<const float4*>(ot + dl * kXT + 4 * c4);
           T* o = out + (((size_t)cur.n * D + cur.dp + dl) * H + cur.y) * (size_t)W + x;
-          const float vv[4] = {v.x, v.y, v.z, v.w};
+          const float vv[4] = {val.x, val.y, val.z, val.w};
 #pragma unroll
           for (int k = 0; k < 4; ++k)
             if (x + k < W) o[k] = from_f<T>(vv[k]);
@@ -310,6 +354,7 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_mfma(
     w = nw;
     c0 = nc0;
     cur = nxt;
+    item = nitem;
   }
 }
 
@@ -337,25 +382,27 @@ template <typename T, int P, int TMAX>
 int launch_band(const void* l, const void* r, void* o, int64_t N, int64_t C, int64_t H, int64_t W,
                 int64_t D, Strides4 ls, Strides4 rs, int divisor, hipStream_t st) {
   constexpr int DMAX = 16 * (TMAX - 1);
+  constexpr int RWMAX = kXT + DMAX;
   const int tiles = (int)ceil_div(W, kXT);
   const int npass = (int)ceil_div(D, DMAX);
   const int64_t nwork = (int64_t)tiles * H * N * npass;
   if (nwork > INT32_MAX) return fail(SM_EINVAL, "inner product: too much work for one launch");
   const int Dp = (int)std::min<int64_t>(D, DMAX);
-  const int Tn = 1 + (Dp - 1 + 15) / 16;
-  const int rwin = kXT + 16 * (Tn - 1);
-  const size_t in_bytes = (size_t)P * (rwin + kXT) * kRowBytes;
+  const size_t in_bytes = (size_t)P * (RWMAX + kXT) * kRowBytes;
   const size_t out_bytes = (size_t)Dp * kXT * 4;
   const size_t shm = std::max(in_bytes, out_bytes);
-  auto kern = ip_band_mfma<T, P, TMAX>;
-  if (shm > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    if (e != hipSuccess)
-      return fail(SM_ELAUNCH, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
-  }
-  // persistent grid: two workgroups per CU (LDS- and register-limited), a multiple of 8
-  int64_t nwg = std::min<int64_t>(nwork, 2 * (int64_t)device_cus());
+  // 4-pixel vector loads need W % 4 == 0 and 4-element-aligned rows on both sides
+  const bool vec = (W % 4 == 0) && ls.n % 4 == 0 && ls.c % 4 == 0 && ls.h % 4 == 0 &&
+                   rs.n % 4 == 0 && rs.c % 4 == 0 && rs.h % 4 == 0 &&
+                   ((reinterpret_cast<uintptr_t>(l) | reinterpret_cast<uintptr_t>(r)) %
+                        (4 * sizeof(T)) == 0);
+  auto kern = vec ? ip_band_mfma<T, P, TMAX, true> : ip_band_mfma<T, P, TMAX, false>;
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+  if (e != hipSuccess)
+    return fail(SM_ELAUNCH, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
+  // persistent grid: one 8-wave workgroup per CU (LDS-limited), a multiple of 8
+  int64_t nwg = std::min<int64_t>(nwork, (int64_t)device_cus());
   nwg = std::max<int64_t>(8, (nwg + 7) / 8 * 8);
   hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(kThreads), shm, st, static_cast<const T*>(l),
                      static_cast<const T*>(r), static_cast<T*>(o), (int)C, (int)H, (int)W, (int)D,
