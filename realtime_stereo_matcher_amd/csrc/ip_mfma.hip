@@ -149,10 +149,10 @@ struct StageItem {
   bool isR, active;
 };
 
-template <typename T, int P, int TMAX, bool VEC>
+template <typename T, int P, int TMAX, bool VEC, bool MEAN>
 __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
     const T* __restrict__ L, const T* __restrict__ R, T* __restrict__ out, int C, int H, int W,
-    int D, Strides4 ls, Strides4 rs, int divisor, int tiles, int npass, int nwork, int ablate) {
+    int D, Strides4 ls, Strides4 rs, int tiles, int npass, int nwork, int ablate) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int DMAX = 16 * (TMAX - 1);
   constexpr int RWMAX = kXT + DMAX;           // window rows at Tn = TMAX
@@ -177,7 +177,7 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
   const int lane = tid & 63;
   const int fr = lane & 15;  // fragment row / column
   const int fk = lane >> 4;  // fragment k-chunk (8 channels)
-  const float fdiv = (float)divisor;
+  const float fdiv = (float)C;  // MEAN: torch divides the channel sum by C
 
   // ---- this thread's staging item: (8-channel chunk, 4-pixel group) of the window or tile
   float v[8][4];  // in-flight item: 8 channels x 4 pixels
@@ -201,16 +201,19 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
       // W % 4 == 0 and j0 % 4 == 0: the 4-pixel group is entirely inside or outside the row
       const bool okj = it.j0 >= 0 && it.j0 < W;
       const int jc = okj ? it.j0 : 0;
+      const bool cfull = cb + 8 <= C;  // wave-uniform
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        const int c = min(cb + k, C - 1);
+        const int c = cfull ? cb + k : min(cb + k, C - 1);
         load4(it.row + (int64_t)c * it.cstride + jc, v[k]);
       }
+      if (!cfull || !__all(okj)) {  // row edges / channel tail only
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const bool ok = okj && (cb + k < C);
+        for (int k = 0; k < 8; ++k) {
+          const bool ok = okj && (cb + k < C);
 #pragma unroll
-        for (int p = 0; p < 4; ++p) v[k][p] = ok ? v[k][p] : 0.f;
+          for (int p = 0; p < 4; ++p) v[k][p] = ok ? v[k][p] : 0.f;
+        }
       }
     } else {
 #pragma unroll
@@ -310,7 +313,8 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
       __syncthreads();
       float* ot = reinterpret_cast<float*>(smem);
       const int xl = 16 * wave + fr;
-      // local disparity of accumulator (t, r): dl = b0 - 16 t - r
+      // local disparity of accumulator (t, r): dl = b0 - 16 t - r.  Elements outside
+      // [0, Dp) go to a trash row (row DMAX) instead of a divergent branch.
       const int b0 = fr - 4 * fk + 16 * (cur.Tn - 1);
       const int j_b = cur.js + 16 * wave + 4 * fk;  // right column of (t = 0, r = 0)
 #pragma unroll
@@ -319,12 +323,11 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int dl = b0 - 16 * t - r;
-            if (dl >= 0 && dl < cur.Dp) {
-              const bool inside = j_b + 16 * t + r >= 0;  // j < 0 <=> x < d: exact zero
-              float val = inside ? acc[t][r] : 0.f;
-              if (divisor >= 0) val = inside ? val / fdiv : 0.f;
-              ot[dl * kXT + xl] = val;
-            }
+            const bool keep = (unsigned)dl < (unsigned)cur.Dp;
+            const bool inside = j_b + 16 * t + r >= 0;  // j < 0 <=> x < d: exact zero
+            float val = acc[t][r];
+            if (MEAN) val = val / fdiv;
+            ot[(keep ? dl : DMAX) * kXT + xl] = inside ? val : 0.f;
           }
         }
       }
@@ -389,14 +392,17 @@ int launch_band(const void* l, const void* r, void* o, int64_t N, int64_t C, int
   if (nwork > INT32_MAX) return fail(SM_EINVAL, "inner product: too much work for one launch");
   const int Dp = (int)std::min<int64_t>(D, DMAX);
   const size_t in_bytes = (size_t)P * (RWMAX + kXT) * kRowBytes;
-  const size_t out_bytes = (size_t)Dp * kXT * 4;
+  const size_t out_bytes = (size_t)(DMAX + 1) * kXT * 4;  // + trash row
   const size_t shm = std::max(in_bytes, out_bytes);
+  (void)Dp;
   // 4-pixel vector loads need W % 4 == 0 and 4-element-aligned rows on both sides
   const bool vec = (W % 4 == 0) && ls.n % 4 == 0 && ls.c % 4 == 0 && ls.h % 4 == 0 &&
                    rs.n % 4 == 0 && rs.c % 4 == 0 && rs.h % 4 == 0 &&
                    ((reinterpret_cast<uintptr_t>(l) | reinterpret_cast<uintptr_t>(r)) %
                         (4 * sizeof(T)) == 0);
-  auto kern = vec ? ip_band_mfma<T, P, TMAX, true> : ip_band_mfma<T, P, TMAX, false>;
+  const bool mean = divisor >= 0;
+  auto kern = vec ? (mean ? ip_band_mfma<T, P, TMAX, true, true> : ip_band_mfma<T, P, TMAX, true, false>)
+                  : (mean ? ip_band_mfma<T, P, TMAX, false, true> : ip_band_mfma<T, P, TMAX, false, false>);
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
   if (e != hipSuccess)
@@ -406,7 +412,7 @@ int launch_band(const void* l, const void* r, void* o, int64_t N, int64_t C, int
   nwg = std::max<int64_t>(8, (nwg + 7) / 8 * 8);
   hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(kThreads), shm, st, static_cast<const T*>(l),
                      static_cast<const T*>(r), static_cast<T*>(o), (int)C, (int)H, (int)W, (int)D,
-                     ls, rs, divisor, tiles, npass, (int)nwork, ablate_bits());
+                     ls, rs, tiles, npass, (int)nwork, ablate_bits());
   return check_launch("ip_band_mfma");
 }
 
