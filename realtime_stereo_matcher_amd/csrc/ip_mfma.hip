@@ -97,6 +97,45 @@ __device__ __forceinline__ void load4(const T* p, float (&o)[4]) {
   }
 }
 
+// ---- LDS-DMA staging (global_load_lds): the next step's raw feature data lands straight in
+// an LDS region with no VGPR destination, issued by inline asm so hipcc does not drain it
+// (or the epilogue's output stores, which vmcnt also counts) at every barrier.  The consumer
+// retires it with a hand-counted s_waitcnt vmcnt(#stores issued after it).
+typedef __attribute__((address_space(3))) unsigned char lds_u8;
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const lds_u8*)p;
+}
+// lanes land at lds_byte + 16 * lane (wave-uniform base in M0)
+__device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_byte) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_byte)
+      : "memory");
+}
+// lanes land at lds_byte + 4 * lane
+__device__ __forceinline__ void glds4(const void* gsrc, unsigned lds_byte) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_byte)
+      : "memory");
+}
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+// raw staging bytes per wave: 8 channels x 64 lanes x 4 pixels
+template <typename T>
+constexpr int raw_wave_bytes() {
+  return 8 * 64 * 4 * (int)sizeof(T);
+}
+
 // 4 consecutive outputs (16-B aligned for fp32, 8-B for 16-bit types) in one store.
 template <typename T>
 __device__ __forceinline__ void store4(T* o, float4 v) {
@@ -159,6 +198,10 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
   constexpr int PLANE_R = RWMAX * kRowBytes;  // compile-time plane strides
   constexpr int PLANE_L = kXT * kRowBytes;
   static_assert((RWMAX + kXT) <= kThreads * 4 / 4, "one staging item per thread");
+  // planes (aliased by the epilogue's [DMAX + 1][128] fp32 tile) | per-wave raw DMA slots
+  constexpr int IN_BYTES = P * (RWMAX + kXT) * kRowBytes;
+  constexpr int OUT_BYTES = (DMAX + 1) * kXT * 4;
+  constexpr int RAW_OFF = IN_BYTES > OUT_BYTES ? IN_BYTES : OUT_BYTES;
   unsigned char* const Rt = smem;
   unsigned char* const Lt = smem + P * PLANE_R;
 
@@ -179,8 +222,15 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
   const int fk = lane >> 4;  // fragment k-chunk (8 channels)
   const float fdiv = (float)C;  // MEAN: torch divides the channel sum by C
 
-  // ---- this thread's staging item: (8-channel chunk, 4-pixel group) of the window or tile
-  float v[8][4];  // in-flight item: 8 channels x 4 pixels
+  // ---- this thread's staging item: (8-channel chunk, 4-pixel group) of the window or tile.
+  // VEC path: the item's 8 channel rows x 4 pixels arrive by LDS-DMA into this wave's raw slot
+  // (lane-linear), issued one step ahead; non-VEC path: plain register loads by the compiler.
+  float v[8][4];
+  bool okj = true, cfull = true;
+  int cbi = 0;
+  unsigned char* const raw_slot = smem + RAW_OFF + wave * raw_wave_bytes<T>();
+  const unsigned raw_lds = __builtin_amdgcn_readfirstlane(lds_addr(smem + RAW_OFF)) +
+                           (unsigned)__builtin_amdgcn_readfirstlane(wave) * raw_wave_bytes<T>();
   auto make_item = [&](const BandWork& k) {
     StageItem<T> it;
     const bool isR = tid < k.rwin;
@@ -196,26 +246,26 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
   };
   auto issue = [&](const StageItem<T>& it, int c0) {
     const int cb = c0 + 8 * it.chunk;
-    if (!it.active) return;
+    cbi = cb;
     if (VEC) {
       // W % 4 == 0 and j0 % 4 == 0: the 4-pixel group is entirely inside or outside the row
-      const bool okj = it.j0 >= 0 && it.j0 < W;
+      okj = it.j0 >= 0 && it.j0 < W;
+      cfull = cb + 8 <= C;
+      if (!it.active) return;  // whole waves only (items end on a 64-lane boundary or later)
       const int jc = okj ? it.j0 : 0;
-      const bool cfull = cb + 8 <= C;  // wave-uniform
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const int c = cfull ? cb + k : min(cb + k, C - 1);
-        load4(it.row + (int64_t)c * it.cstride + jc, v[k]);
-      }
-      if (!cfull || !__all(okj)) {  // row edges / channel tail only
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const bool ok = okj && (cb + k < C);
-#pragma unroll
-          for (int p = 0; p < 4; ++p) v[k][p] = ok ? v[k][p] : 0.f;
+        const T* src = it.row + (int64_t)c * it.cstride + jc;
+        if constexpr (sizeof(T) == 4) {
+          glds16(src, raw_lds + k * 1024);
+        } else {
+          glds4(src, raw_lds + k * 512);
+          glds4(src + 2, raw_lds + k * 512 + 256);
         }
       }
     } else {
+      if (!it.active) return;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const int c = min(cb + k, C - 1);
@@ -229,8 +279,44 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
       }
     }
   };
-  auto stage = [&](const StageItem<T>& it) {
+  auto stage = [&](const StageItem<T>& it, bool after_epilogue) {
+    if (VEC) {
+      // retire this wave's LDS-DMA; only the epilogue's DMAX/16 row stores may stay in flight
+      if (after_epilogue)
+        vm_wait<DMAX / 16>();
+      else
+        vm_wait<0>();
+    }
     if (!it.active) return;
+    if (VEC && C > 0) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        if constexpr (sizeof(T) == 4) {
+          const float4 f = *reinterpret_cast<const float4*>(raw_slot + k * 1024 + 16 * lane);
+          v[k][0] = f.x;
+          v[k][1] = f.y;
+          v[k][2] = f.z;
+          v[k][3] = f.w;
+        } else {
+          union {
+            unsigned u[2];
+            T e[4];
+          } q;
+          q.u[0] = *reinterpret_cast<const unsigned*>(raw_slot + k * 512 + 4 * lane);
+          q.u[1] = *reinterpret_cast<const unsigned*>(raw_slot + k * 512 + 256 + 4 * lane);
+#pragma unroll
+          for (int p = 0; p < 4; ++p) v[k][p] = to_f(q.e[p]);
+        }
+      }
+      if (!cfull || !__all(okj)) {  // row edges / channel tail only
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const bool ok = okj && (cbi + k < C);
+#pragma unroll
+          for (int p = 0; p < 4; ++p) v[k][p] = ok ? v[k][p] : 0.f;
+        }
+      }
+    }
     unsigned char* base = it.isR ? Rt : Lt;
     const int pstride = it.isR ? PLANE_R : PLANE_L;
 #pragma unroll
@@ -250,18 +336,17 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
   BandWork cur = band_decode(w, tiles, npass, H, D, DMAX);
   StageItem<T> item = make_item(cur);
   int c0 = 0;
-  if (C <= 0 || (ablate & 2)) {  // empty channel axis: zero sum (mean: 0/0 = NaN, as torch)
+  bool counted_epi = false;  // the previous step ended with exactly DMAX/16 full-row stores
+  const bool no_hbm = (ablate & 2) != 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
+  for (int k = 0; k < 8; ++k)
 #pragma unroll
-      for (int p = 0; p < 4; ++p) v[k][p] = 0.f;
-  } else {
-    issue(item, 0);
-  }
+    for (int p = 0; p < 4; ++p) v[k][p] = 0.f;  // C == 0: zero sum (mean: 0/0 = NaN, as torch)
+  if (C > 0) issue(item, 0);
 
   while (true) {
     __syncthreads();  // previous fragment reads / out-tile reads are done
-    stage(item);
+    stage(item, counted_epi);
     __syncthreads();
 
     // prefetch the next (segment, channel step) before this step's MFMAs and epilogue
@@ -271,7 +356,7 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
     const bool has_next = nw < wend;
     const BandWork nxt = last_step ? band_decode(has_next ? nw : w, tiles, npass, H, D, DMAX) : cur;
     const StageItem<T> nitem = last_step ? make_item(nxt) : item;
-    if (has_next && !(ablate & 2)) issue(nitem, nc0);
+    if (C > 0 && has_next && !no_hbm) issue(nitem, nc0);
 
     if (c0 == 0) {
 #pragma unroll
@@ -337,6 +422,13 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
       const bool fullrow = (cur.x0 + kXT <= W) && ((W & 3) == 0);
       if (ablate & 4) {
         // diagnostic path: no output stream
+      } else if (fullrow && cur.Dp == DMAX) {  // the counted case: DMAX/16 stores per lane
+#pragma unroll
+        for (int it16 = 0; it16 < DMAX / 16; ++it16) {
+          const int dl = (tid >> 5) + 16 * it16;
+          const float4 val = *reinterpret_cast<const float4*>(ot + dl * kXT + 4 * c4);
+          store4(out + (((size_t)cur.n * D + cur.dp + dl) * H + cur.y) * (size_t)W + x, val);
+        }
       } else if (fullrow) {  // 16-B aligned row segments: one wide store per lane per row
         for (int dl = tid >> 5; dl < cur.Dp; dl += kThreads / 32) {
           const float4 val = *reinterpret_cast<const float4*>(ot + dl * kXT + 4 * c4);
@@ -353,6 +445,8 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
         }
       }
     }
+    counted_epi = last_step && !(ablate & 4) && cur.Dp == DMAX && (cur.x0 + kXT <= W) &&
+                  ((W & 3) == 0);
     if (!has_next) break;
     w = nw;
     c0 = nc0;
@@ -393,7 +487,8 @@ int launch_band(const void* l, const void* r, void* o, int64_t N, int64_t C, int
   const int Dp = (int)std::min<int64_t>(D, DMAX);
   const size_t in_bytes = (size_t)P * (RWMAX + kXT) * kRowBytes;
   const size_t out_bytes = (size_t)(DMAX + 1) * kXT * 4;  // + trash row
-  const size_t shm = std::max(in_bytes, out_bytes);
+  const int item_waves = (RWMAX + kXT + 63) / 64;
+  const size_t shm = std::max(in_bytes, out_bytes) + (size_t)item_waves * raw_wave_bytes<T>();
   (void)Dp;
   // 4-pixel vector loads need W % 4 == 0 and 4-element-aligned rows on both sides
   const bool vec = (W % 4 == 0) && ls.n % 4 == 0 && ls.c % 4 == 0 && ls.h % 4 == 0 &&
@@ -422,7 +517,8 @@ int launch_band_d(const void* l, const void* r, void* o, int64_t N, int64_t C, i
   if (D <= 64) return launch_band<T, P, 5>(l, r, o, N, C, H, W, D, ls, rs, divisor, st);
   if (D <= 128) return launch_band<T, P, 9>(l, r, o, N, C, H, W, D, ls, rs, divisor, st);
   if (D <= 192) return launch_band<T, P, 13>(l, r, o, N, C, H, W, D, ls, rs, divisor, st);
-  return launch_band<T, P, 17>(l, r, o, N, C, H, W, D, ls, rs, divisor, st);
+  // D > 192: passes of 128 disparities (the 192-wide tile plus DMA slots would exceed LDS)
+  return launch_band<T, P, 9>(l, r, o, N, C, H, W, D, ls, rs, divisor, st);
 }
 
 }  // namespace
