@@ -32,9 +32,39 @@
 #include <cstdlib>
 
 namespace smcv {
-namespace {
+namespace band {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// Diagnostic phase stamps (scripts/ip_stamps.hip builds this file with -DSMCV_STAMPS; the
+// library never does).  Each wave accumulates s_memtime deltas per phase.
+#ifdef SMCV_STAMPS
+constexpr int kStampPhases = 8;
+__device__ unsigned long long g_stamps[4096][kStampPhases];
+#define SM_STAMP_DECL                              \
+  unsigned long long st_acc[kStampPhases] = {0};   \
+  unsigned long long st_t = __builtin_amdgcn_s_memtime();
+#define SM_STAMP(ph)                                           \
+  do {                                                         \
+    __builtin_amdgcn_sched_barrier(0);                         \
+    const unsigned long long st_n = __builtin_amdgcn_s_memtime(); \
+    st_acc[ph] += st_n - st_t;                                 \
+    st_t = st_n;                                               \
+    __builtin_amdgcn_sched_barrier(0);                         \
+  } while (0)
+#define SM_STAMP_FLUSH                                                         \
+  if ((threadIdx.x & 63) == 0) {                                               \
+    const int gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);        \
+    if (gw < 4096)                                                             \
+      for (int ph = 0; ph < kStampPhases; ++ph) g_stamps[gw][ph] = st_acc[ph]; \
+  }
+#else
+#define SM_STAMP_DECL
+#define SM_STAMP(ph) \
+  do {               \
+  } while (0)
+#define SM_STAMP_FLUSH
+#endif
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kWaves = 8;
@@ -344,10 +374,14 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
     for (int p = 0; p < 4; ++p) v[k][p] = 0.f;  // C == 0: zero sum (mean: 0/0 = NaN, as torch)
   if (C > 0) issue(item, 0);
 
+  SM_STAMP_DECL
   while (true) {
     __syncthreads();  // previous fragment reads / out-tile reads are done
+    SM_STAMP(0);
     stage(item, counted_epi);
+    SM_STAMP(1);
     __syncthreads();
+    SM_STAMP(2);
 
     // prefetch the next (segment, channel step) before this step's MFMAs and epilogue
     const bool last_step = c0 + kKC >= C;
@@ -393,9 +427,11 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
       }
     }
 
+    SM_STAMP(3);
     if (last_step) {
       // ---- epilogue: shear S[j][x] -> out[d = x - j][x] through an LDS [Dp][128] fp32 tile
       __syncthreads();
+      SM_STAMP(4);
       float* ot = reinterpret_cast<float*>(smem);
       const int xl = 16 * wave + fr;
       // local disparity of accumulator (t, r): dl = b0 - 16 t - r.  Elements outside
@@ -416,7 +452,9 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
           }
         }
       }
+      SM_STAMP(5);
       __syncthreads();
+      SM_STAMP(6);
       const int c4 = tid & 31;
       const int x = cur.x0 + 4 * c4;
       const bool fullrow = (cur.x0 + kXT <= W) && ((W & 3) == 0);
@@ -447,12 +485,14 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
     }
     counted_epi = last_step && !(ablate & 4) && cur.Dp == DMAX && (cur.x0 + kXT <= W) &&
                   ((W & 3) == 0);
+    if (last_step) SM_STAMP(7);
     if (!has_next) break;
     w = nw;
     c0 = nc0;
     cur = nxt;
     item = nitem;
   }
+  SM_STAMP_FLUSH
 }
 
 // Diagnostic ablation bits (STEREOCV_ABLATE, timing studies only; outputs become garbage):
@@ -521,7 +561,9 @@ int launch_band_d(const void* l, const void* r, void* o, int64_t N, int64_t C, i
   return launch_band<T, P, 9>(l, r, o, N, C, H, W, D, ls, rs, divisor, st);
 }
 
-}  // namespace
+}  // namespace band
+
+using namespace band;
 
 int check_dot_args(const void* left, const void* right, const void* out, int dtype, int64_t N,
                    int64_t C, int64_t H, int64_t W, int64_t D, const int64_t* l_strides,

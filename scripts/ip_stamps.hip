@@ -1,0 +1,59 @@
+// Diagnostic driver: per-phase s_memtime breakdown of the inner-product band kernel
+// (cfg2 shape).  Build + run on the GPU box:
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -DSMCV_STAMPS -Iinclude scripts/ip_stamps.hip -o /tmp/ip_stamps && /tmp/ip_stamps
+// Stamps execute only in this build (never in libstereocv.so).
+#include "../realtime_stereo_matcher_amd/csrc/common.hip"
+#include "../realtime_stereo_matcher_amd/csrc/cv_dot.hip"
+#include "../realtime_stereo_matcher_amd/csrc/ip_mfma.hip"
+
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+int main(int argc, char** argv) {
+  const int64_t N = 1, C = 64, H = 540, W = 960, D = argc > 1 ? atoi(argv[1]) : 192;
+  const size_t nin = N * C * H * W, nout = N * D * H * W;
+  float *L, *R, *O;
+  hipMalloc(&L, nin * 4);
+  hipMalloc(&R, nin * 4);
+  hipMalloc(&O, nout * 4);
+  std::vector<float> h(nin);
+  for (size_t i = 0; i < nin; ++i) h[i] = (float)((i * 2654435761u) % 2001) / 1000.f - 1.f;
+  hipMemcpy(L, h.data(), nin * 4, hipMemcpyHostToDevice);
+  hipMemcpy(R, h.data(), nin * 4, hipMemcpyHostToDevice);
+  for (int it = 0; it < 3; ++it)
+    smcv::band_mfma_entry(L, R, O, SM_F32, N, C, H, W, D, nullptr, nullptr, 0, nullptr);
+  hipDeviceSynchronize();
+  static unsigned long long zero[4096][8];
+  memset(zero, 0, sizeof(zero));
+  hipMemcpyToSymbol(HIP_SYMBOL(smcv::g_stamps), zero, sizeof(zero));
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  hipEventRecord(a);
+  int rc = smcv::band_mfma_entry(L, R, O, SM_F32, N, C, H, W, D, nullptr, nullptr, 0, nullptr);
+  hipEventRecord(b);
+  hipEventSynchronize(b);
+  float ms = 0;
+  hipEventElapsedTime(&ms, a, b);
+  static unsigned long long st[4096][8];
+  hipMemcpyFromSymbol(st, HIP_SYMBOL(smcv::g_stamps), sizeof(st));
+  const char* names[8] = {"top barrier", "stage (wait+split+lds)", "stage barrier", "dma issue + mfma",
+                          "epi barrier 1", "shear writes", "epi barrier 2", "store loop"};
+  double sum[8] = {0};
+  int nw = 0;
+  for (int w = 0; w < 4096; ++w) {
+    unsigned long long t = 0;
+    for (int p = 0; p < 8; ++p) t += st[w][p];
+    if (!t) continue;
+    ++nw;
+    for (int p = 0; p < 8; ++p) sum[p] += st[w][p];
+  }
+  double tot = 0;
+  for (int p = 0; p < 8; ++p) tot += sum[p];
+  printf("rc=%d kernel %.1f us, %d waves with stamps\n", rc, ms * 1e3, nw);
+  for (int p = 0; p < 8; ++p)
+    printf("  %-26s %10.0f cycles/wave  %5.1f %%\n", names[p], sum[p] / nw, 100.0 * sum[p] / tot);
+  printf("  total %.0f cycles/wave\n", tot / nw);
+  return 0;
+}
