@@ -127,6 +127,23 @@ __device__ __forceinline__ void load4(const T* p, float (&o)[4]) {
   }
 }
 
+// acc += A * B over the P-plane split: for P = 3 the six products l*h, m*m, h*l, m*h, h*m, h*h
+// (smallest first); P = 2: m*m, m*h, h*m, h*h (exact for fp16 data); P = 1: h*h.
+template <int P>
+__device__ __forceinline__ void band_mma(f32x4& acc, const bf16x8 (&a)[P], const bf16x8 (&b)[P]) {
+  if constexpr (P == 3) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], acc, 0, 0, 0);
+  }
+  if constexpr (P == 2) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], acc, 0, 0, 0);
+  if constexpr (P >= 2) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], acc, 0, 0, 0);
+  }
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc, 0, 0, 0);
+}
+
 // ---- LDS-DMA staging (global_load_lds): the next step's raw feature data lands straight in
 // an LDS region with no VGPR destination, issued by inline asm so hipcc does not drain it
 // (or the epilogue's output stores, which vmcnt also counts) at every barrier.  The consumer
@@ -160,11 +177,13 @@ __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
 }
 
-// raw staging bytes per wave: 8 channels x 64 lanes x 4 pixels
+// staging items (8 channels x 4 pixels) per wave for a TMAX-block band, and the raw LDS-DMA
+// bytes one wave needs for them: 8 channel blocks of IPW lanes x 4 pixels
+constexpr int band_ipw(int tmax) { return ((16 * 8 + 16 * (tmax - 1) + 16 * 8) / 8 + 3) / 4 * 4; }
 template <typename T>
-constexpr int raw_wave_bytes() {
-  return 8 * 64 * 4 * (int)sizeof(T);
-}
+constexpr int raw_k_bytes(int tmax) { return band_ipw(tmax) * 4 * (int)sizeof(T); }
+template <typename T>
+constexpr int raw_wave_bytes(int tmax) { return 8 * raw_k_bytes<T>(tmax); }
 
 // 4 consecutive outputs (16-B aligned for fp32, 8-B for 16-bit types) in one store.
 template <typename T>
@@ -227,11 +246,14 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
   constexpr int RWMAX = kXT + DMAX;           // window rows at Tn = TMAX
   constexpr int PLANE_R = RWMAX * kRowBytes;  // compile-time plane strides
   constexpr int PLANE_L = kXT * kRowBytes;
-  static_assert((RWMAX + kXT) <= kThreads * 4 / 4, "one staging item per thread");
+  constexpr int IPW = band_ipw(TMAX);  // staging items per wave
+  constexpr int RAWK = raw_k_bytes<T>(TMAX);
+  static_assert(IPW == ((RWMAX + kXT) / kWaves + 3) / 4 * 4, "band_ipw mismatch");
+  static_assert(IPW <= 64 && IPW * kWaves >= RWMAX + kXT, "one staging item per lane");
   // planes (aliased by the epilogue's [DMAX + 1][128] fp32 tile) | per-wave raw DMA slots
   constexpr int IN_BYTES = P * (RWMAX + kXT) * kRowBytes;
   constexpr int OUT_BYTES = (DMAX + 1) * kXT * 4;
-  constexpr int RAW_OFF = IN_BYTES > OUT_BYTES ? IN_BYTES : OUT_BYTES;
+  constexpr int RAW_OFF = IN_BYTES > OUT_BYTES ? IN_BYTES : OUT_BYTES;  // + 8 raw slots
   unsigned char* const Rt = smem;
   unsigned char* const Lt = smem + P * PLANE_R;
 
@@ -258,15 +280,18 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
   float v[8][4];
   bool okj = true, cfull = true;
   int cbi = 0;
-  unsigned char* const raw_slot = smem + RAW_OFF + wave * raw_wave_bytes<T>();
+  unsigned char* const raw_slot = smem + RAW_OFF + wave * raw_wave_bytes<T>(TMAX);
   const unsigned raw_lds = __builtin_amdgcn_readfirstlane(lds_addr(smem + RAW_OFF)) +
-                           (unsigned)__builtin_amdgcn_readfirstlane(wave) * raw_wave_bytes<T>();
+                           (unsigned)__builtin_amdgcn_readfirstlane(wave) * raw_wave_bytes<T>(TMAX);
+  // items are dealt in contiguous blocks of IPW per wave so every wave stages the same amount
+  // (lanes >= IPW idle); within a wave, consecutive lanes walk pixel groups of one row
+  const int item_id = wave * IPW + lane;
   auto make_item = [&](const BandWork& k) {
     StageItem<T> it;
-    const bool isR = tid < k.rwin;
-    const int i = isR ? tid : tid - k.rwin;
+    const bool isR = item_id < k.rwin;
+    const int i = isR ? item_id : item_id - k.rwin;
     it.isR = isR;
-    it.active = tid < k.rwin + kXT;
+    it.active = lane < IPW && item_id < k.rwin + kXT;
     it.chunk = i & 3;
     it.lrow = 4 * (i >> 2);
     it.j0 = (isR ? k.js : k.x0) + it.lrow;
@@ -288,10 +313,10 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
         const int c = cfull ? cb + k : min(cb + k, C - 1);
         const T* src = it.row + (int64_t)c * it.cstride + jc;
         if constexpr (sizeof(T) == 4) {
-          glds16(src, raw_lds + k * 1024);
+          glds16(src, raw_lds + k * RAWK);
         } else {
-          glds4(src, raw_lds + k * 512);
-          glds4(src + 2, raw_lds + k * 512 + 256);
+          glds4(src, raw_lds + k * RAWK);
+          glds4(src + 2, raw_lds + k * RAWK + RAWK / 2);
         }
       }
     } else {
@@ -322,7 +347,7 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         if constexpr (sizeof(T) == 4) {
-          const float4 f = *reinterpret_cast<const float4*>(raw_slot + k * 1024 + 16 * lane);
+          const float4 f = *reinterpret_cast<const float4*>(raw_slot + k * RAWK + 16 * lane);
           v[k][0] = f.x;
           v[k][1] = f.y;
           v[k][2] = f.z;
@@ -332,8 +357,8 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
             unsigned u[2];
             T e[4];
           } q;
-          q.u[0] = *reinterpret_cast<const unsigned*>(raw_slot + k * 512 + 4 * lane);
-          q.u[1] = *reinterpret_cast<const unsigned*>(raw_slot + k * 512 + 256 + 4 * lane);
+          q.u[0] = *reinterpret_cast<const unsigned*>(raw_slot + k * RAWK + 4 * lane);
+          q.u[1] = *reinterpret_cast<const unsigned*>(raw_slot + k * RAWK + RAWK / 2 + 4 * lane);
 #pragma unroll
           for (int p = 0; p < 4; ++p) v[k][p] = to_f(q.e[p]);
         }
@@ -397,32 +422,46 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
       for (int t = 0; t < TMAX; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
 
-    // ---- band MMA: B = left x-block (cols x), A = right j-block (rows j)
+    // ---- band MMA: B = left x-block (cols x), A = right j-block (rows j).  The full band
+    // (Tn == TMAX, every work item but the last pass of a D > DMAX split) runs a compile-time
+    // loop that reads block t+1's fragments while block t's six MFMAs issue.
     if (!(ablate & 1)) {
       bf16x8 bq[P];
       const int boff = swz(16 * wave + fr, fk);
 #pragma unroll
       for (int p = 0; p < P; ++p) bq[p] = *reinterpret_cast<const bf16x8*>(Lt + p * PLANE_L + boff);
-      const int aoff = swz(16 * wave + fr, fk);  // + 1024 * t (the swizzle is 16-row periodic)
+      const unsigned char* abase = Rt + swz(16 * wave + fr, fk);  // + 1024 t: 16-row periodic
+      if (cur.Tn == TMAX) {
+        bf16x8 a0[P], a1[P];
 #pragma unroll
-      for (int t = 0; t < TMAX; ++t) {
-        if (t < cur.Tn) {
-          bf16x8 aq[P];
+        for (int p = 0; p < P; ++p) a0[p] = *reinterpret_cast<const bf16x8*>(abase + p * PLANE_R);
 #pragma unroll
-          for (int p = 0; p < P; ++p)
-            aq[p] = *reinterpret_cast<const bf16x8*>(Rt + p * PLANE_R + aoff + 1024 * t);
-          if (P == 3) {
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[2], bq[0], acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[1], bq[1], acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[0], bq[2], acc[t], 0, 0, 0);
+        for (int t = 0; t < TMAX; t += 2) {
+          if (t + 1 < TMAX) {
+#pragma unroll
+            for (int p = 0; p < P; ++p)
+              a1[p] = *reinterpret_cast<const bf16x8*>(abase + p * PLANE_R + 1024 * (t + 1));
           }
-          if (P >= 2) {
-            if (P == 2)
-              acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[1], bq[1], acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[1], bq[0], acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[0], bq[1], acc[t], 0, 0, 0);
+          band_mma<P>(acc[t], a0, bq);
+          if (t + 1 < TMAX) {
+            if (t + 2 < TMAX) {
+#pragma unroll
+              for (int p = 0; p < P; ++p)
+                a0[p] = *reinterpret_cast<const bf16x8*>(abase + p * PLANE_R + 1024 * (t + 2));
+            }
+            band_mma<P>(acc[t + 1], a1, bq);
           }
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[0], bq[0], acc[t], 0, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < TMAX; ++t) {
+          if (t < cur.Tn) {
+            bf16x8 aq[P];
+#pragma unroll
+            for (int p = 0; p < P; ++p)
+              aq[p] = *reinterpret_cast<const bf16x8*>(abase + p * PLANE_R + 1024 * t);
+            band_mma<P>(acc[t], aq, bq);
+          }
         }
       }
     }
@@ -438,17 +477,37 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
       // [0, Dp) go to a trash row (row DMAX) instead of a divergent branch.
       const int b0 = fr - 4 * fk + 16 * (cur.Tn - 1);
       const int j_b = cur.js + 16 * wave + 4 * fk;  // right column of (t = 0, r = 0)
+      float* const olane = ot + b0 * kXT + xl;      // element (t, r) at olane - (16t + r) * kXT
+      if (cur.Tn == TMAX && cur.Dp == DMAX && cur.js >= 0) {
+        // interior segment: only the first and last band blocks straddle [0, DMAX)
 #pragma unroll
-      for (int t = 0; t < TMAX; ++t) {
-        if (t < cur.Tn) {
+        for (int t = 0; t < TMAX; ++t) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int dl = b0 - 16 * t - r;
-            const bool keep = (unsigned)dl < (unsigned)cur.Dp;
-            const bool inside = j_b + 16 * t + r >= 0;  // j < 0 <=> x < d: exact zero
             float val = acc[t][r];
             if (MEAN) val = val / fdiv;
-            ot[(keep ? dl : DMAX) * kXT + xl] = inside ? val : 0.f;
+            if (t == 0 || t == TMAX - 1) {
+              const int dl = b0 - 16 * t - r;
+              const bool keep = (unsigned)dl < (unsigned)DMAX;
+              ot[(keep ? dl : DMAX) * kXT + xl] = val;
+            } else {
+              olane[-(16 * t + r) * kXT] = val;
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < TMAX; ++t) {
+          if (t < cur.Tn) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int dl = b0 - 16 * t - r;
+              const bool keep = (unsigned)dl < (unsigned)cur.Dp;
+              const bool inside = j_b + 16 * t + r >= 0;  // j < 0 <=> x < d: exact zero
+              float val = acc[t][r];
+              if (MEAN) val = val / fdiv;
+              ot[(keep ? dl : DMAX) * kXT + xl] = inside ? val : 0.f;
+            }
           }
         }
       }
@@ -527,8 +586,7 @@ int launch_band(const void* l, const void* r, void* o, int64_t N, int64_t C, int
   const int Dp = (int)std::min<int64_t>(D, DMAX);
   const size_t in_bytes = (size_t)P * (RWMAX + kXT) * kRowBytes;
   const size_t out_bytes = (size_t)(DMAX + 1) * kXT * 4;  // + trash row
-  const int item_waves = (RWMAX + kXT + 63) / 64;
-  const size_t shm = std::max(in_bytes, out_bytes) + (size_t)item_waves * raw_wave_bytes<T>();
+  const size_t shm = std::max(in_bytes, out_bytes) + (size_t)kWaves * raw_wave_bytes<T>(TMAX);
   (void)Dp;
   // 4-pixel vector loads need W % 4 == 0 and 4-element-aligned rows on both sides
   const bool vec = (W % 4 == 0) && ls.n % 4 == 0 && ls.c % 4 == 0 && ls.h % 4 == 0 &&
