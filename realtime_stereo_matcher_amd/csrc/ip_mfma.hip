@@ -39,8 +39,9 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 // Diagnostic phase stamps (scripts/ip_stamps.hip builds this file with -DSMCV_STAMPS; the
 // library never does).  Each wave accumulates s_memtime deltas per phase.
 #ifdef SMCV_STAMPS
-constexpr int kStampPhases = 8;
+constexpr int kStampPhases = 12;
 __device__ unsigned long long g_stamps[4096][kStampPhases];
+#define SM_STAMP_IN(ph) SM_STAMP(ph)
 #define SM_STAMP_DECL                              \
   unsigned long long st_acc[kStampPhases] = {0};   \
   unsigned long long st_t = __builtin_amdgcn_s_memtime();
@@ -64,6 +65,9 @@ __device__ unsigned long long g_stamps[4096][kStampPhases];
   do {               \
   } while (0)
 #define SM_STAMP_FLUSH
+#define SM_STAMP_IN(ph) \
+  do {                  \
+  } while (0)
 #endif
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -273,6 +277,7 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
   const int fr = lane & 15;  // fragment row / column
   const int fk = lane >> 4;  // fragment k-chunk (8 channels)
   const float fdiv = (float)C;  // MEAN: torch divides the channel sum by C
+  SM_STAMP_DECL
 
   // ---- this thread's staging item: (8-channel chunk, 4-pixel group) of the window or tile.
   // VEC path: the item's 8 channel rows x 4 pixels arrive by LDS-DMA into this wave's raw slot
@@ -342,6 +347,7 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
       else
         vm_wait<0>();
     }
+    SM_STAMP_IN(8);
     if (!it.active) return;
     if (VEC && C > 0) {
 #pragma unroll
@@ -399,7 +405,6 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
     for (int p = 0; p < 4; ++p) v[k][p] = 0.f;  // C == 0: zero sum (mean: 0/0 = NaN, as torch)
   if (C > 0) issue(item, 0);
 
-  SM_STAMP_DECL
   while (true) {
     __syncthreads();  // previous fragment reads / out-tile reads are done
     SM_STAMP(0);
@@ -416,6 +421,7 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
     const BandWork nxt = last_step ? band_decode(has_next ? nw : w, tiles, npass, H, D, DMAX) : cur;
     const StageItem<T> nitem = last_step ? make_item(nxt) : item;
     if (C > 0 && has_next && !no_hbm) issue(nitem, nc0);
+    SM_STAMP(9);
 
     if (c0 == 0) {
 #pragma unroll

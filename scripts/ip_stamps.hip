@@ -24,7 +24,7 @@ int main(int argc, char** argv) {
   for (int it = 0; it < 3; ++it)
     smcv::band_mfma_entry(L, R, O, SM_F32, N, C, H, W, D, nullptr, nullptr, 0, nullptr);
   hipDeviceSynchronize();
-  static unsigned long long zero[4096][8];
+  static unsigned long long zero[4096][12];
   memset(zero, 0, sizeof(zero));
   hipMemcpyToSymbol(HIP_SYMBOL(smcv::g_stamps), zero, sizeof(zero));
   hipEvent_t a, b;
@@ -36,23 +36,24 @@ int main(int argc, char** argv) {
   hipEventSynchronize(b);
   float ms = 0;
   hipEventElapsedTime(&ms, a, b);
-  static unsigned long long st[4096][8];
+  static unsigned long long st[4096][12];
   hipMemcpyFromSymbol(st, HIP_SYMBOL(smcv::g_stamps), sizeof(st));
-  const char* names[8] = {"top barrier", "stage (wait+split+lds)", "stage barrier", "dma issue + mfma",
-                          "epi barrier 1", "shear writes", "epi barrier 2", "store loop"};
-  double sum[8] = {0};
+  const char* names[12] = {"top barrier", "stage (split+lds)", "stage barrier", "mfma",
+                           "epi barrier 1", "shear writes", "epi barrier 2", "store loop",
+                           "stage: dma wait", "dma issue", "-", "-"};
+  double sum[12] = {0};
   int nw = 0;
   for (int w = 0; w < 4096; ++w) {
     unsigned long long t = 0;
-    for (int p = 0; p < 8; ++p) t += st[w][p];
+    for (int p = 0; p < 12; ++p) t += st[w][p];
     if (!t) continue;
     ++nw;
-    for (int p = 0; p < 8; ++p) sum[p] += st[w][p];
+    for (int p = 0; p < 12; ++p) sum[p] += st[w][p];
   }
   double tot = 0;
-  for (int p = 0; p < 8; ++p) tot += sum[p];
+  for (int p = 0; p < 12; ++p) tot += sum[p];
   printf("rc=%d kernel %.1f us, %d waves with stamps\n", rc, ms * 1e3, nw);
-  for (int p = 0; p < 8; ++p)
+  for (int p = 0; p < 10; ++p)
     printf("  %-26s %10.0f cycles/wave  %5.1f %%\n", names[p], sum[p] / nw, 100.0 * sum[p] / tot);
   printf("  total %.0f cycles/wave\n", tot / nw);
   return 0;
