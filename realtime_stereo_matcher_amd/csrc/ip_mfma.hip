@@ -304,28 +304,35 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
     it.cstride = isR ? rs.c : ls.c;
     return it;
   };
-  auto issue = [&](const StageItem<T>& it, int c0) {
+  // VEC: issue_prep() latches the item's DMA source; issue_piece(k) sends channel k of the
+  // item (one LDS-DMA wave instruction).  The eight pieces are spread over the MFMA stream.
+  const T* dma_src = L;
+  int64_t dma_cs = 0;
+  bool dma_on = false;
+  auto issue_piece = [&](int k) {
+    if (VEC && dma_on) {
+      const int c = cfull ? cbi + k : min(cbi + k, C - 1);
+      const T* src = dma_src + (int64_t)c * dma_cs;
+      if constexpr (sizeof(T) == 4) {
+        glds16(src, raw_lds + k * RAWK);
+      } else {
+        glds4(src, raw_lds + k * RAWK);
+        glds4(src + 2, raw_lds + k * RAWK + RAWK / 2);
+      }
+    }
+  };
+  auto issue_prep = [&](const StageItem<T>& it, int c0, bool on) {
     const int cb = c0 + 8 * it.chunk;
     cbi = cb;
     if (VEC) {
       // W % 4 == 0 and j0 % 4 == 0: the 4-pixel group is entirely inside or outside the row
       okj = it.j0 >= 0 && it.j0 < W;
       cfull = cb + 8 <= C;
-      if (!it.active) return;  // whole waves only (items end on a 64-lane boundary or later)
-      const int jc = okj ? it.j0 : 0;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int c = cfull ? cb + k : min(cb + k, C - 1);
-        const T* src = it.row + (int64_t)c * it.cstride + jc;
-        if constexpr (sizeof(T) == 4) {
-          glds16(src, raw_lds + k * RAWK);
-        } else {
-          glds4(src, raw_lds + k * RAWK);
-          glds4(src + 2, raw_lds + k * RAWK + RAWK / 2);
-        }
-      }
+      dma_on = on && it.active;
+      dma_src = it.row + (okj ? it.j0 : 0);
+      dma_cs = it.cstride;
     } else {
-      if (!it.active) return;
+      if (!on || !it.active) return;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const int c = min(cb + k, C - 1);
@@ -338,6 +345,11 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
         }
       }
     }
+  };
+  auto issue = [&](const StageItem<T>& it, int c0) {
+    issue_prep(it, c0, true);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) issue_piece(k);
   };
   auto stage = [&](const StageItem<T>& it, bool after_epilogue) {
     if (VEC) {
@@ -420,7 +432,14 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
     const bool has_next = nw < wend;
     const BandWork nxt = last_step ? band_decode(has_next ? nw : w, tiles, npass, H, D, DMAX) : cur;
     const StageItem<T> nitem = last_step ? make_item(nxt) : item;
-    if (C > 0 && has_next && !no_hbm) issue(nitem, nc0);
+    // the next step's DMA: latched here, its 8 pieces interleaved with the band blocks below
+    const bool dma_next = C > 0 && has_next && !no_hbm;
+    issue_prep(nitem, nc0, dma_next);
+    const bool interleave = VEC && cur.Tn == TMAX && !(ablate & 1);
+    if (!interleave) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) issue_piece(k);
+    }
     SM_STAMP(9);
 
     if (c0 == 0) {
@@ -449,6 +468,9 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
               a1[p] = *reinterpret_cast<const bf16x8*>(abase + p * PLANE_R + 1024 * (t + 1));
           }
           band_mma<P>(acc[t], a0, bq);
+#pragma unroll
+          for (int k = (8 * t + TMAX - 1) / TMAX; k < (8 * (t + 1) + TMAX - 1) / TMAX; ++k)
+            issue_piece(k);  // DMA pieces spread evenly over the band blocks
           if (t + 1 < TMAX) {
             if (t + 2 < TMAX) {
 #pragma unroll
@@ -456,6 +478,9 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_mfma(
                 a0[p] = *reinterpret_cast<const bf16x8*>(abase + p * PLANE_R + 1024 * (t + 2));
             }
             band_mma<P>(acc[t + 1], a1, bq);
+#pragma unroll
+            for (int k = (8 * (t + 1) + TMAX - 1) / TMAX; k < (8 * (t + 2) + TMAX - 1) / TMAX; ++k)
+              issue_piece(k);
           }
         }
       } else {
