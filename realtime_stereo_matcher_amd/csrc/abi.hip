@@ -9,6 +9,9 @@ int dot_volume_valu_entry(const void* left, const void* right, void* out, int dt
 int band_mfma_entry(const void* left, const void* right, void* out, int dtype, int64_t N, int64_t C,
                     int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
                     const int64_t* r_strides, int mode, void* stream);
+int band_f32_entry(const void* left, const void* right, void* out, int dtype, int64_t N,
+                   int64_t C, int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
+                   const int64_t* r_strides, int mode, void* stream, bool* handled);
 int ip_mfma_entry(const void* left, const void* right, void* out, int dtype, int64_t N,
                   int64_t C, int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
                   const int64_t* r_strides, void* stream, bool* handled);
@@ -36,18 +39,27 @@ extern "C" int sm_cv_inner_product_ex(const void* left, const void* right, void*
                                       const int64_t* l_strides, const int64_t* r_strides,
                                       int algo, void* stream) {
   SM_ENTRY_BEGIN
-  if (algo != SM_IP_AUTO && algo != SM_IP_VALU && algo != SM_IP_MFMA_F32)
-    return fail(SM_EINVAL, "unknown inner-product algo");
-  if (algo == SM_IP_AUTO || algo == SM_IP_MFMA_F32) {
-    bool handled = false;
-    int rc = ip_mfma_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, stream,
-                           &handled);
-    if (handled || rc != SM_OK) return rc;
-    if (algo == SM_IP_MFMA_F32)
-      return fail(SM_EINVAL, "MFMA inner product does not support this shape/dtype");
+  switch (algo) {
+    case SM_IP_AUTO:
+    case SM_IP_MFMA_F32: {
+      // fp32: exact fp32 MFMA band kernel; 16-bit inputs (and shapes the DMA path cannot
+      // take) go to the bf16-split band kernel
+      bool handled = false;
+      int rc = band_f32_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
+                              stream, &handled);
+      if (handled || rc != SM_OK) return rc;
+      return band_mfma_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
+                             stream);
+    }
+    case SM_IP_MFMA_BF16X3:
+      return band_mfma_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
+                             stream);
+    case SM_IP_VALU:
+      return dot_volume_valu_entry(left, right, out, dtype, N, C, H, W, D, 1, l_strides,
+                                   r_strides, 0, stream);
+    default:
+      return fail(SM_EINVAL, "unknown inner-product algo");
   }
-  return dot_volume_valu_entry(left, right, out, dtype, N, C, H, W, D, 1, l_strides, r_strides,
-                               0, stream);
 }
 
 extern "C" int sm_cv_inner_product(const void* left, const void* right, void* out, int dtype,
@@ -63,6 +75,10 @@ extern "C" int sm_cv_correlation_mean(const void* left, const void* right, void*
                                       const int64_t* l_strides, const int64_t* r_strides,
                                       void* stream) {
   SM_ENTRY_BEGIN
+  bool handled = false;
+  int rc = band_f32_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 1, stream,
+                          &handled);
+  if (handled || rc != SM_OK) return rc;
   return band_mfma_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 1, stream);
 }
 
