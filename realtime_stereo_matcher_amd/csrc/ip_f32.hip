@@ -177,25 +177,43 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_f32(
     const float* Lb = Rb + G::RGROUPS * 4;
     const float* aL = Rb + fk * G::RROW + 16 * wave + fr;  // + s*4*RROW + 16 t
     const float* bL = Lb + fk * kLRow + 16 * wave + fr;    // + s*4*kLRow
-    auto mma = [&](auto full_tag) {
-      constexpr bool FULL = decltype(full_tag)::value;
+    // full band: all 13 A values (+ B) of k-step s+1 are read into registers before the 13
+    // MFMAs of k-step s issue (sched_barrier keeps the order), so the LDS latency of a read
+    // hides behind a whole k-step instead of being waited for per MFMA
+    auto kread = [&](int s, float (&av)[TMAX], float& bv) {
+      bv = bL[s * 4 * kLRow];
+      bv = (c0 + 4 * s + fk < C) ? bv : 0.f;  // channels past C contribute nothing
+#pragma unroll
+      for (int t = 0; t < TMAX; ++t) av[t] = aL[s * 4 * G::RROW + 16 * t];
+    };
+    if (cur.Tn == TMAX) {
+      float a0[TMAX], a1[TMAX], b0, b1;
+      kread(0, a0, b0);
+#pragma unroll
+      for (int s = 0; s < kKC / 4; s += 2) {
+        kread(s + 1, a1, b1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < TMAX; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[t], b0, acc[t], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (s + 2 < kKC / 4) kread(s + 2, a0, b0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < TMAX; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[t], b1, acc[t], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
 #pragma unroll
       for (int s = 0; s < kKC / 4; ++s) {
-        float bv = bL[s * 4 * kLRow];
-        bv = (c0 + 4 * s + fk < C) ? bv : 0.f;  // channels past C contribute nothing
+        float av[TMAX], bv;
+        kread(s, av, bv);
 #pragma unroll
-        for (int t = 0; t < TMAX; ++t) {
-          if (FULL || t < cur.Tn) {
-            const float av = aL[s * 4 * G::RROW + 16 * t];
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[t], 0, 0, 0);
-          }
-        }
+        for (int t = 0; t < TMAX; ++t)
+          if (t < cur.Tn) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t], bv, acc[t], 0, 0, 0);
       }
-    };
-    if (cur.Tn == TMAX)
-      mma(std::true_type{});
-    else
-      mma(std::false_type{});
+    }
 
     if (last_step) {
       // ---- epilogue: shear S[j][x] -> out[d = x - j][x] through the LDS [Dp][128] tile
