@@ -117,6 +117,7 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_f32(
   const int fk = lane >> 4;
   const unsigned smem_lds = __builtin_amdgcn_readfirstlane(lds_addr(smem));
   const int uwave = __builtin_amdgcn_readfirstlane(wave);
+  SM_STAMP_DECL
 
   // issue this wave's DMA pieces of (work k, channel step c0) into stage buffer b
   auto issue = [&](const Work& k, int c0, int b) {
@@ -158,7 +159,9 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_f32(
       vm_wait<DMAX / 16>();
     else
       vm_wait<0>();
+    SM_STAMP(8);
     __syncthreads();
+    SM_STAMP(0);
 
     const bool last_step = c0 + kKC >= C;
     const int nw = last_step ? w + gsz : w;
@@ -166,6 +169,7 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_f32(
     const bool has_next = nw < wend;
     const Work nxt = last_step ? decode(has_next ? nw : w, tiles, npass, H, D, DMAX) : cur;
     if (has_next) issue(nxt, nc0, buf ^ 1);  // the other buffer: free since the barrier
+    SM_STAMP(9);
 
     if (c0 == 0) {
 #pragma unroll
@@ -215,6 +219,7 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_f32(
       }
     }
 
+    SM_STAMP(3);
     if (last_step) {
       // ---- epilogue: shear S[j][x] -> out[d = x - j][x] through the LDS [Dp][128] tile
       const int xl = 16 * wave + fr;
@@ -254,7 +259,9 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_f32(
           }
         }
       }
+      SM_STAMP(5);
       __syncthreads();
+      SM_STAMP(6);
       const int c4 = tid & 31;
       const int x = cur.x0 + 4 * c4;
       const bool fullrow = (cur.x0 + kXT <= W) && ((W & 3) == 0);
@@ -278,6 +285,7 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_f32(
       }
       // the out tile is rewritten only after the next segment's steps (>= 1 barrier away)
     }
+    if (last_step) SM_STAMP(7);
     counted_epi = last_step && cur.Dp == DMAX && (cur.x0 + kXT <= W) && ((W & 3) == 0);
     if (!has_next) break;
     w = nw;
@@ -285,6 +293,7 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_f32(
     cur = nxt;
     buf ^= 1;
   }
+  SM_STAMP_FLUSH
 }
 
 int device_cus() {

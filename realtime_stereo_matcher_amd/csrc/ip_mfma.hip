@@ -36,39 +36,7 @@ namespace band {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-// Diagnostic phase stamps (scripts/ip_stamps.hip builds this file with -DSMCV_STAMPS; the
-// library never does).  Each wave accumulates s_memtime deltas per phase.
-#ifdef SMCV_STAMPS
-constexpr int kStampPhases = 12;
-__device__ unsigned long long g_stamps[4096][kStampPhases];
-#define SM_STAMP_IN(ph) SM_STAMP(ph)
-#define SM_STAMP_DECL                              \
-  unsigned long long st_acc[kStampPhases] = {0};   \
-  unsigned long long st_t = __builtin_amdgcn_s_memtime();
-#define SM_STAMP(ph)                                           \
-  do {                                                         \
-    __builtin_amdgcn_sched_barrier(0);                         \
-    const unsigned long long st_n = __builtin_amdgcn_s_memtime(); \
-    st_acc[ph] += st_n - st_t;                                 \
-    st_t = st_n;                                               \
-    __builtin_amdgcn_sched_barrier(0);                         \
-  } while (0)
-#define SM_STAMP_FLUSH                                                         \
-  if ((threadIdx.x & 63) == 0) {                                               \
-    const int gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);        \
-    if (gw < 4096)                                                             \
-      for (int ph = 0; ph < kStampPhases; ++ph) g_stamps[gw][ph] = st_acc[ph]; \
-  }
-#else
-#define SM_STAMP_DECL
-#define SM_STAMP(ph) \
-  do {               \
-  } while (0)
-#define SM_STAMP_FLUSH
-#define SM_STAMP_IN(ph) \
-  do {                  \
-  } while (0)
-#endif
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kWaves = 8;

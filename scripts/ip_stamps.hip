@@ -5,6 +5,11 @@
 #include "../realtime_stereo_matcher_amd/csrc/common.hip"
 #include "../realtime_stereo_matcher_amd/csrc/cv_dot.hip"
 #include "../realtime_stereo_matcher_amd/csrc/ip_mfma.hip"
+#include "../realtime_stereo_matcher_amd/csrc/ip_f32.hip"
+
+namespace smcv {
+__device__ unsigned long long g_stamps[4096][kStampPhases];
+}
 
 #include <cstdio>
 #include <cstring>
@@ -17,12 +22,18 @@ int main(int argc, char** argv) {
   hipMalloc(&L, nin * 4);
   hipMalloc(&R, nin * 4);
   hipMalloc(&O, nout * 4);
+  const bool f32 = argc > 2 && !strcmp(argv[2], "f32");
+  bool handled = false;
+  auto run = [&]() {
+    if (f32) return smcv::band_f32_entry(L, R, O, SM_F32, N, C, H, W, D, nullptr, nullptr, 0, nullptr, &handled);
+    return smcv::band_mfma_entry(L, R, O, SM_F32, N, C, H, W, D, nullptr, nullptr, 0, nullptr);
+  };
   std::vector<float> h(nin);
   for (size_t i = 0; i < nin; ++i) h[i] = (float)((i * 2654435761u) % 2001) / 1000.f - 1.f;
   hipMemcpy(L, h.data(), nin * 4, hipMemcpyHostToDevice);
   hipMemcpy(R, h.data(), nin * 4, hipMemcpyHostToDevice);
   for (int it = 0; it < 3; ++it)
-    smcv::band_mfma_entry(L, R, O, SM_F32, N, C, H, W, D, nullptr, nullptr, 0, nullptr);
+    run();
   hipDeviceSynchronize();
   static unsigned long long zero[4096][12];
   memset(zero, 0, sizeof(zero));
@@ -31,7 +42,7 @@ int main(int argc, char** argv) {
   hipEventCreate(&a);
   hipEventCreate(&b);
   hipEventRecord(a);
-  int rc = smcv::band_mfma_entry(L, R, O, SM_F32, N, C, H, W, D, nullptr, nullptr, 0, nullptr);
+  int rc = run();
   hipEventRecord(b);
   hipEventSynchronize(b);
   float ms = 0;
@@ -41,6 +52,7 @@ int main(int argc, char** argv) {
   const char* names[12] = {"top barrier", "stage (split+lds)", "stage barrier", "mfma",
                            "epi barrier 1", "shear writes", "epi barrier 2", "store loop",
                            "stage: dma wait", "dma issue", "-", "-"};
+  printf("kernel: %s\n", f32 ? "f32 band" : "bf16x3 band");
   double sum[12] = {0};
   int nw = 0;
   for (int w = 0; w < 4096; ++w) {
