@@ -8,7 +8,7 @@ disparity regression (model/mobile_disp_net_c.py:208-220).  A STEP is one pass o
 path over the rank's batch of pairs (inputs already resident in HBM), plus -- for N>1 -- the
 RCCL gather of the per-pair disparities to rank 0 (the only collective).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--algo auto|valu|mfma]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--algo auto|bf16x3|f32|valu]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
 Rank 0 prints ONE JSON line.  ``value`` = pairs processed by all ranks / max-over-ranks wall
@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=1, help="stereo pairs per GPU per step")
-    ap.add_argument("--algo", default="auto", choices=["auto", "valu", "mfma"])
+    ap.add_argument("--algo", default="auto", choices=["auto", "bf16x3", "f32", "mfma", "valu"])
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
                     help="bounded CPU-baseline sample length (0 disables)")
     return ap.parse_args()
@@ -145,7 +145,9 @@ def main():
 
     cv_ms = sum(s.elapsed_time(e) for s, e in ev) / max(1, len(ev))
     achieved = cv_algorithmic_bytes(B) / (cv_ms * 1e-3) / 1e9
-    traffic = traffic_from_profiles("dot_volume" if a.algo == "valu" else "ip_")
+    kname = {"valu": "dot_volume_valu", "f32": "ip_band_f32", "mfma": "ip_band_f32"}.get(
+        a.algo, "ip_band_mfma")
+    traffic = traffic_from_profiles(kname)
     pairs = global_batch * a.steps
     rec = {
         "metric": "stereo pairs/sec (KITTI-res 540x960x64 inner-product cost volume D=192 + soft-argmin)",
@@ -167,7 +169,7 @@ def main():
                    "parallelism": f"dp{world}", "algo": a.algo},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "inner-product cost volume", "avg_kernel_us": cv_ms * 1e3,
+                     "kernel": kname, "avg_kernel_us": cv_ms * 1e3,
                      "algorithmic_bytes_per_launch": cv_algorithmic_bytes(B)},
     }
     if rank == 0 and world == 1 and a.cpu_baseline_seconds > 0:

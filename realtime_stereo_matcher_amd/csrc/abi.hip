@@ -40,10 +40,9 @@ extern "C" int sm_cv_inner_product_ex(const void* left, const void* right, void*
                                       int algo, void* stream) {
   SM_ENTRY_BEGIN
   switch (algo) {
-    case SM_IP_AUTO:
     case SM_IP_MFMA_F32: {
-      // fp32: exact fp32 MFMA band kernel; 16-bit inputs (and shapes the DMA path cannot
-      // take) go to the bf16-split band kernel
+      // exact fp32 MFMA band kernel; shapes the DMA path cannot take go to the bf16-split
+      // band kernel
       bool handled = false;
       int rc = band_f32_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
                               stream, &handled);
@@ -51,6 +50,7 @@ extern "C" int sm_cv_inner_product_ex(const void* left, const void* right, void*
       return band_mfma_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
                              stream);
     }
+    case SM_IP_AUTO:  // the bf16-split band kernel is the faster one on gfx950
     case SM_IP_MFMA_BF16X3:
       return band_mfma_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
                              stream);
@@ -75,10 +75,6 @@ extern "C" int sm_cv_correlation_mean(const void* left, const void* right, void*
                                       const int64_t* l_strides, const int64_t* r_strides,
                                       void* stream) {
   SM_ENTRY_BEGIN
-  bool handled = false;
-  int rc = band_f32_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 1, stream,
-                          &handled);
-  if (handled || rc != SM_OK) return rc;
   return band_mfma_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 1, stream);
 }
 

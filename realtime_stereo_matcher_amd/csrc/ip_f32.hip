@@ -120,27 +120,31 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_f32(
   SM_STAMP_DECL
 
   // issue this wave's DMA pieces of (work k, channel step c0) into stage buffer b
+  // Kernel-argument strides are copied to plain (SGPR) scalars first: selecting a struct
+  // member per lane made hipcc fetch it with a VMEM load + vmcnt(0), draining every DMA piece
+  // and output store in flight.
+  const int64_t rsn = rs.n, rsc = rs.c, rsh = rs.h, lsn = ls.n, lsc = ls.c, lsh = ls.h;
   auto issue = [&](const Work& k, int c0, int b) {
-    const float* Rrow = R + k.n * rs.n + (int64_t)k.y * rs.h;
-    const float* Lrow = L + k.n * ls.n + (int64_t)k.y * ls.h;
+    const float* Rrow = R + k.n * rsn + (int64_t)k.y * rsh;
+    const float* Lrow = L + k.n * lsn + (int64_t)k.y * lsh;
 #pragma unroll
     for (int pp = 0; pp < G::PPW; ++pp) {
       const int piece = uwave + kWaves * pp;
-      if (piece < G::PIECES) {
+      if (piece < G::PIECES) {  // wave-uniform
         const int g = piece * 64 + lane;
-        const float* src;
-        if (g < G::RGROUPS) {
-          const int row = g / (G::RROW / 4);
-          const int px = 4 * (g - row * (G::RROW / 4));  // pad positions fetch valid junk
-          const int j = min(max(k.js + px, 0), W - 4);
-          src = Rrow + (int64_t)min(c0 + row, C - 1) * rs.c + j;
-        } else {
-          const int gl = min(g - G::RGROUPS, G::LGROUPS - 1);
-          const int row = gl / (kLRow / 4);
-          const int px = 4 * (gl - row * (kLRow / 4));
-          const int x = min(k.x0 + px, W - 4);
-          src = Lrow + (int64_t)min(c0 + row, C - 1) * ls.c + x;
-        }
+        const bool isR = g < G::RGROUPS;
+        // right window: row of RROW/4 groups; pad positions fetch valid junk
+        const int rrow = g / (G::RROW / 4);
+        const int rpx = 4 * (g - rrow * (G::RROW / 4));
+        const int j = min(max(k.js + rpx, 0), W - 4);
+        // left tile
+        const int gl = min(max(g - G::RGROUPS, 0), G::LGROUPS - 1);
+        const int lrow = gl / (kLRow / 4);
+        const int lpx = 4 * (gl - lrow * (kLRow / 4));
+        const int x = min(k.x0 + lpx, W - 4);
+        const int64_t roff = (int64_t)min(c0 + rrow, C - 1) * rsc + j;
+        const int64_t loff = (int64_t)min(c0 + lrow, C - 1) * lsc + x;
+        const float* src = isR ? Rrow + roff : Lrow + loff;
         glds16(src, smem_lds + (unsigned)(b * G::BUF_FLOATS + piece * 256) * 4);
       }
     }
