@@ -36,7 +36,7 @@ def _ids(cs):
 
 
 # =============================================================================== golden vectors
-@pytest.mark.parametrize("algo", ["auto", "bf16x3", "valu"])
+@pytest.mark.parametrize("algo", ["auto", "bf16x3", "f32", "valu"])
 @pytest.mark.parametrize("rec", cases("inner_product"), ids=_ids(cases("inner_product")))
 def test_golden_inner_product(rec, algo):
     from realtime_stereo_matcher_amd.cost_volume import TorchInnerProductCost
@@ -190,7 +190,7 @@ def _feats(seed, shape, kind="normal"):
     return rng.standard_normal(shape, dtype=np.float32), rng.standard_normal(shape, dtype=np.float32)
 
 
-@pytest.mark.parametrize("algo", ["auto", "bf16x3", "valu"])
+@pytest.mark.parametrize("algo", ["auto", "bf16x3", "f32", "valu"])
 @pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
 def test_inner_product_vs_oracle(shape, algo):
     from realtime_stereo_matcher_amd import functional as F
@@ -312,7 +312,7 @@ def _rows_check(full, fn_oracle, rows, atol, exact=False):
             np.testing.assert_allclose(got, want, atol=atol, rtol=0)
 
 
-@pytest.mark.parametrize("algo", ["auto", "bf16x3", "valu"])
+@pytest.mark.parametrize("algo", ["auto", "bf16x3", "f32", "valu"])
 def test_cfg2_inner_product_full_size(algo):
     """BASELINE configs[1]: 1x64x540x960 fp32, D=192 -- every row depends only on the same
     row of L and R (inner_product.py:38-40), so rows sampled from the full-size launch are
