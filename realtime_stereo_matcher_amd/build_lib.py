@@ -22,6 +22,11 @@ CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", os.pat
             "-Wall", "-Wno-unused-function", "-munsafe-fp-atomics"]
 
 
+# per-source extra flags: the warp-specialised band kernel keeps scalar f32 VALU next to its
+# MFMAs (SLP-packed v_pk_add_f32 issue slower there: MI355X_MICROARCH.md, filler prices)
+EXTRA = {"ip_ws.hip": ["-fno-slp-vectorize"]}
+
+
 def hipcc():
     for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
         if cand and os.path.exists(cand):
@@ -39,7 +44,7 @@ def _compile(src):
     deps.append(os.path.join(ROOT, "include", "stereocv.h"))
     if os.path.exists(obj) and all(os.path.getmtime(obj) >= os.path.getmtime(d) for d in deps):
         return obj
-    cmd = [hipcc(), *CXXFLAGS, "-c", src, "-o", obj]
+    cmd = [hipcc(), *CXXFLAGS, *EXTRA.get(os.path.basename(src), []), "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed on {src}:\n{r.stdout}\n{r.stderr}")

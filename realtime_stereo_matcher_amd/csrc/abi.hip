@@ -12,6 +12,9 @@ int band_mfma_entry(const void* left, const void* right, void* out, int dtype, i
 int band_f32_entry(const void* left, const void* right, void* out, int dtype, int64_t N,
                    int64_t C, int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
                    const int64_t* r_strides, int mode, void* stream, bool* handled);
+int band_ws_entry(const void* left, const void* right, void* out, int dtype, int64_t N, int64_t C,
+                  int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
+                  const int64_t* r_strides, int mode, void* stream, bool* handled);
 int ip_mfma_entry(const void* left, const void* right, void* out, int dtype, int64_t N,
                   int64_t C, int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
                   const int64_t* r_strides, void* stream, bool* handled);
@@ -50,7 +53,15 @@ extern "C" int sm_cv_inner_product_ex(const void* left, const void* right, void*
       return band_mfma_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
                              stream);
     }
-    case SM_IP_AUTO:  // the bf16-split band kernel is the faster one on gfx950
+    case SM_IP_AUTO:  // fp32: the warp-specialised split kernel; otherwise the bf16-split one
+    case SM_IP_MFMA_WS: {
+      bool handled = false;
+      int rc = band_ws_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
+                             stream, &handled);
+      if (handled || rc != SM_OK) return rc;
+      return band_mfma_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
+                             stream);
+    }
     case SM_IP_MFMA_BF16X3:
       return band_mfma_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
                              stream);
@@ -75,6 +86,10 @@ extern "C" int sm_cv_correlation_mean(const void* left, const void* right, void*
                                       const int64_t* l_strides, const int64_t* r_strides,
                                       void* stream) {
   SM_ENTRY_BEGIN
+  bool handled = false;
+  int rc = band_ws_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 1, stream,
+                         &handled);
+  if (handled || rc != SM_OK) return rc;
   return band_mfma_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 1, stream);
 }
 

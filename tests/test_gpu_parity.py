@@ -36,7 +36,7 @@ def _ids(cs):
 
 
 # =============================================================================== golden vectors
-@pytest.mark.parametrize("algo", ["auto", "bf16x3", "f32", "valu"])
+@pytest.mark.parametrize("algo", ["auto", "ws", "bf16x3", "f32", "valu"])
 @pytest.mark.parametrize("rec", cases("inner_product"), ids=_ids(cases("inner_product")))
 def test_golden_inner_product(rec, algo):
     from realtime_stereo_matcher_amd.cost_volume import TorchInnerProductCost
@@ -169,7 +169,7 @@ def test_golden_argext(rec):
     fn = F.hard_argmax if rec["params"]["mode"] == "max" else F.hard_argmin
     np.testing.assert_array_equal(host(fn(dev(a["volume"]))), a["out"])
     if "left" in a:  # end to end: integer features -> exact volume -> bit-exact argmax
-        for algo in ("auto", "bf16x3", "valu"):
+        for algo in ("auto", "ws", "bf16x3", "f32", "valu"):
             vol = TorchInnerProductCost(rec["params"]["max_disparity"], algo=algo)(dev(a["left"]), dev(a["right"]))
             np.testing.assert_array_equal(host(vol), a["volume"])
             np.testing.assert_array_equal(host(F.hard_argmax(vol)), a["out"])
@@ -179,6 +179,9 @@ def test_golden_argext(rec):
 SHAPES = [  # (N, C, H, W, D)
     (1, 1, 1, 1, 1), (1, 3, 2, 7, 5), (2, 17, 3, 65, 24), (1, 64, 2, 200, 192), (1, 16, 3, 130, 256),
     (1, 32, 2, 100, 300), (1, 8, 2, 64, 64), (1, 5, 1, 33, 0), (3, 64, 1, 97, 65), (1, 128, 2, 70, 48),
+    # W % 4 == 0 shapes for the 16-B staging paths: channel tails, partial bands, D passes, W < 128
+    (2, 20, 3, 260, 100), (1, 48, 2, 132, 33), (1, 16, 1, 1000, 256), (1, 7, 2, 36, 40),
+    (1, 64, 2, 960, 192), (1, 33, 2, 512, 31),
 ]
 
 
@@ -190,7 +193,7 @@ def _feats(seed, shape, kind="normal"):
     return rng.standard_normal(shape, dtype=np.float32), rng.standard_normal(shape, dtype=np.float32)
 
 
-@pytest.mark.parametrize("algo", ["auto", "bf16x3", "f32", "valu"])
+@pytest.mark.parametrize("algo", ["auto", "ws", "bf16x3", "f32", "valu"])
 @pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
 def test_inner_product_vs_oracle(shape, algo):
     from realtime_stereo_matcher_amd import functional as F
@@ -204,7 +207,7 @@ def test_inner_product_vs_oracle(shape, algo):
                                   O.inner_product(li, ri, D))
 
 
-@pytest.mark.parametrize("shape", SHAPES[:7], ids=[str(s) for s in SHAPES[:7]])
+@pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
 def test_correlation_and_groupwise_vs_oracle(shape):
     from realtime_stereo_matcher_amd import functional as F
 
@@ -312,7 +315,7 @@ def _rows_check(full, fn_oracle, rows, atol, exact=False):
             np.testing.assert_allclose(got, want, atol=atol, rtol=0)
 
 
-@pytest.mark.parametrize("algo", ["auto", "bf16x3", "f32", "valu"])
+@pytest.mark.parametrize("algo", ["auto", "ws", "bf16x3", "f32", "valu"])
 def test_cfg2_inner_product_full_size(algo):
     """BASELINE configs[1]: 1x64x540x960 fp32, D=192 -- every row depends only on the same
     row of L and R (inner_product.py:38-40), so rows sampled from the full-size launch are
