@@ -15,6 +15,9 @@ int band_f32_entry(const void* left, const void* right, void* out, int dtype, in
 int band_ws_entry(const void* left, const void* right, void* out, int dtype, int64_t N, int64_t C,
                   int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
                   const int64_t* r_strides, int mode, void* stream, bool* handled);
+int band_h2_entry(const void* left, const void* right, void* out, int dtype, int64_t N, int64_t C,
+                  int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
+                  const int64_t* r_strides, int mode, void* stream, bool* handled);
 int ip_mfma_entry(const void* left, const void* right, void* out, int dtype, int64_t N,
                   int64_t C, int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
                   const int64_t* r_strides, void* stream, bool* handled);
@@ -53,7 +56,15 @@ extern "C" int sm_cv_inner_product_ex(const void* left, const void* right, void*
       return band_mfma_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
                              stream);
     }
-    case SM_IP_AUTO:  // fp32: the warp-specialised split kernel; otherwise the bf16-split one
+    case SM_IP_AUTO:  // fp32: the two-plane fp16 kernel; otherwise the bf16-split one
+    case SM_IP_MFMA_H2: {
+      bool handled = false;
+      int rc = band_h2_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
+                             stream, &handled);
+      if (handled || rc != SM_OK) return rc;
+      return band_mfma_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
+                             stream);
+    }
     case SM_IP_MFMA_WS: {
       bool handled = false;
       int rc = band_ws_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
@@ -87,7 +98,7 @@ extern "C" int sm_cv_correlation_mean(const void* left, const void* right, void*
                                       void* stream) {
   SM_ENTRY_BEGIN
   bool handled = false;
-  int rc = band_ws_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 1, stream,
+  int rc = band_h2_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 1, stream,
                          &handled);
   if (handled || rc != SM_OK) return rc;
   return band_mfma_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 1, stream);

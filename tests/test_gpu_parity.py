@@ -36,7 +36,7 @@ def _ids(cs):
 
 
 # =============================================================================== golden vectors
-@pytest.mark.parametrize("algo", ["auto", "ws", "bf16x3", "f32", "valu"])
+@pytest.mark.parametrize("algo", ["auto", "h2", "ws", "bf16x3", "f32", "valu"])
 @pytest.mark.parametrize("rec", cases("inner_product"), ids=_ids(cases("inner_product")))
 def test_golden_inner_product(rec, algo):
     from realtime_stereo_matcher_amd.cost_volume import TorchInnerProductCost
@@ -169,7 +169,7 @@ def test_golden_argext(rec):
     fn = F.hard_argmax if rec["params"]["mode"] == "max" else F.hard_argmin
     np.testing.assert_array_equal(host(fn(dev(a["volume"]))), a["out"])
     if "left" in a:  # end to end: integer features -> exact volume -> bit-exact argmax
-        for algo in ("auto", "ws", "bf16x3", "f32", "valu"):
+        for algo in ("auto", "h2", "ws", "bf16x3", "f32", "valu"):
             vol = TorchInnerProductCost(rec["params"]["max_disparity"], algo=algo)(dev(a["left"]), dev(a["right"]))
             np.testing.assert_array_equal(host(vol), a["volume"])
             np.testing.assert_array_equal(host(F.hard_argmax(vol)), a["out"])
@@ -193,7 +193,7 @@ def _feats(seed, shape, kind="normal"):
     return rng.standard_normal(shape, dtype=np.float32), rng.standard_normal(shape, dtype=np.float32)
 
 
-@pytest.mark.parametrize("algo", ["auto", "ws", "bf16x3", "f32", "valu"])
+@pytest.mark.parametrize("algo", ["auto", "h2", "ws", "bf16x3", "f32", "valu"])
 @pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
 def test_inner_product_vs_oracle(shape, algo):
     from realtime_stereo_matcher_amd import functional as F
@@ -315,7 +315,7 @@ def _rows_check(full, fn_oracle, rows, atol, exact=False):
             np.testing.assert_allclose(got, want, atol=atol, rtol=0)
 
 
-@pytest.mark.parametrize("algo", ["auto", "ws", "bf16x3", "f32", "valu"])
+@pytest.mark.parametrize("algo", ["auto", "h2", "ws", "bf16x3", "f32", "valu"])
 def test_cfg2_inner_product_full_size(algo):
     """BASELINE configs[1]: 1x64x540x960 fp32, D=192 -- every row depends only on the same
     row of L and R (inner_product.py:38-40), so rows sampled from the full-size launch are
