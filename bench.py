@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=1, help="stereo pairs per GPU per step")
-    ap.add_argument("--algo", default="auto", choices=["auto", "h2", "ws", "bf16x3", "f32", "mfma", "valu"])
+    ap.add_argument("--algo", default="auto", choices=["auto", "h2", "bf16x3", "f32", "mfma", "valu"])
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
                     help="bounded CPU-baseline sample length (0 disables)")
     return ap.parse_args()
@@ -146,7 +146,7 @@ def main():
     cv_ms = sum(s.elapsed_time(e) for s, e in ev) / max(1, len(ev))
     achieved = cv_algorithmic_bytes(B) / (cv_ms * 1e-3) / 1e9
     kname = {"valu": "dot_volume_valu", "f32": "ip_band_f32", "mfma": "ip_band_f32",
-             "ws": "ip_band_ws", "bf16x3": "ip_band_mfma"}.get(a.algo, "ip_band_h2")
+             "bf16x3": "ip_band_mfma"}.get(a.algo, "ip_band_h2")
     traffic = traffic_from_profiles(kname)
     pairs = global_batch * a.steps
     rec = {

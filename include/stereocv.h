@@ -40,10 +40,10 @@ enum sm_ip_algo {
   SM_IP_VALU = 1,        /* fp32 VALU, LDS-staged right window reused across the D sweep */
   SM_IP_MFMA_F32 = 2,    /* banded C-contraction on v_mfma_f32_16x16x4_f32 (exact fp32 fma) */
   SM_IP_MFMA_BF16X3 = 3, /* banded C-contraction on bf16 MFMA over an exact 3-way bf16 split */
-  SM_IP_MFMA_WS = 4,     /* the same split on 32x32x16 bf16 MFMA, warp-specialised (stage waves
-                            split into LDS while math waves run the MFMAs); fp32 only */
-  SM_IP_MFMA_H2 = 5      /* fp32 default: per-segment power-of-two scale + exact-range-checked
-                            two-plane fp16 split on 32x32x16 f16 MFMA, two workgroups per CU */
+  /* 4: reserved (a retired warp-specialised variant of the bf16 split) */
+  SM_IP_MFMA_H2 = 5      /* default: per-segment power-of-two scale + range-checked two-plane
+                            fp16 split on 32x32x16 f16 MFMA, two workgroups per CU; segments
+                            holding +-inf take an exact fp32 path (any input dtype) */
 };
 
 /* Library version (major*10000 + minor*100 + patch). */

@@ -22,9 +22,8 @@ CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", os.pat
             "-Wall", "-Wno-unused-function", "-munsafe-fp-atomics"]
 
 
-# per-source extra flags: the warp-specialised band kernel keeps scalar f32 VALU next to its
-# MFMAs (SLP-packed v_pk_add_f32 issue slower there: MI355X_MICROARCH.md, filler prices)
-EXTRA = {"ip_ws.hip": ["-fno-slp-vectorize"]}
+# per-source extra flags (none at present)
+EXTRA = {}
 
 
 def hipcc():

@@ -12,9 +12,6 @@ int band_mfma_entry(const void* left, const void* right, void* out, int dtype, i
 int band_f32_entry(const void* left, const void* right, void* out, int dtype, int64_t N,
                    int64_t C, int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
                    const int64_t* r_strides, int mode, void* stream, bool* handled);
-int band_ws_entry(const void* left, const void* right, void* out, int dtype, int64_t N, int64_t C,
-                  int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
-                  const int64_t* r_strides, int mode, void* stream, bool* handled);
 int band_h2_entry(const void* left, const void* right, void* out, int dtype, int64_t N, int64_t C,
                   int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
                   const int64_t* r_strides, int mode, void* stream, bool* handled);
@@ -47,31 +44,22 @@ extern "C" int sm_cv_inner_product_ex(const void* left, const void* right, void*
   SM_ENTRY_BEGIN
   switch (algo) {
     case SM_IP_MFMA_F32: {
-      // exact fp32 MFMA band kernel; shapes the DMA path cannot take go to the bf16-split
-      // band kernel
+      // exact fp32 MFMA band kernel; shapes the DMA path cannot take go to the VALU kernel
       bool handled = false;
       int rc = band_f32_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
                               stream, &handled);
       if (handled || rc != SM_OK) return rc;
-      return band_mfma_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
-                             stream);
+      return dot_volume_valu_entry(left, right, out, dtype, N, C, H, W, D, 1, l_strides,
+                                   r_strides, 0, stream);
     }
-    case SM_IP_AUTO:  // fp32: the two-plane fp16 kernel; otherwise the bf16-split one
+    case SM_IP_AUTO:  // the two-plane fp16 band kernel; odd shapes: the exact VALU kernel
     case SM_IP_MFMA_H2: {
       bool handled = false;
       int rc = band_h2_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
                              stream, &handled);
       if (handled || rc != SM_OK) return rc;
-      return band_mfma_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
-                             stream);
-    }
-    case SM_IP_MFMA_WS: {
-      bool handled = false;
-      int rc = band_ws_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
-                             stream, &handled);
-      if (handled || rc != SM_OK) return rc;
-      return band_mfma_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
-                             stream);
+      return dot_volume_valu_entry(left, right, out, dtype, N, C, H, W, D, 1, l_strides,
+                                   r_strides, 0, stream);
     }
     case SM_IP_MFMA_BF16X3:
       return band_mfma_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
@@ -101,7 +89,8 @@ extern "C" int sm_cv_correlation_mean(const void* left, const void* right, void*
   int rc = band_h2_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 1, stream,
                          &handled);
   if (handled || rc != SM_OK) return rc;
-  return band_mfma_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 1, stream);
+  return dot_volume_valu_entry(left, right, out, dtype, N, C, H, W, D, 1, l_strides, r_strides,
+                               1, stream);
 }
 
 extern "C" int sm_cv_groupwise(const void* left, const void* right, float* out, int dtype,

@@ -59,7 +59,9 @@ constexpr int kRowB = 32;           // bytes per plane row: 16 fp16
 constexpr int kSlot = 32 * 512;     // one ring chunk: 32 output rows x 128 px fp32
 constexpr int kRing = 3 * kSlot;
 
-// byte offset of (plane row r, 8-channel chunk h); see ip_ws.hip / scripts/check_swizzle.py
+// byte offset of (plane row r, 8-channel chunk h).  Fragment reads: lane l -> row base + (l & 31),
+// chunk l >> 5; plane writes: 8 consecutive lanes -> rows 4i + p of one 32-row block.  Both are
+// conflict-free under the gfx950 ds_read_b128 / ds_write_b128 lane groups (scripts/check_swizzle.py).
 __device__ __forceinline__ int swz(int r, int h) {
   return ((r ^ ((r >> 2) & 3)) << 5) + ((h ^ ((r >> 4) & 1)) << 4);
 }
@@ -114,6 +116,44 @@ __device__ __forceinline__ __attribute__((address_space(3))) unsigned* lds_word(
   return reinterpret_cast<__attribute__((address_space(3))) unsigned*>(addr);
 }
 
+// a 4-pixel group of one channel row in registers: 16 B (fp32) or 8 B (fp16 / bf16)
+template <typename T> struct Quad { using type = uint2; };
+template <> struct Quad<float> { using type = float4; };
+
+template <typename T>
+__device__ __forceinline__ float4 quad_to_f32(typename Quad<T>::type q) {
+  if constexpr (sizeof(T) == 4) {
+    return q;
+  } else if constexpr (std::is_same<T, __half>::value) {
+    const hp2 a = __builtin_bit_cast(hp2, q.x), b = __builtin_bit_cast(hp2, q.y);
+    return make_float4((float)a[0], (float)a[1], (float)b[0], (float)b[1]);
+  } else {  // bf16: the value is the high half of an fp32
+    return make_float4(__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u),
+                       __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u));
+  }
+}
+
+// 4 fp32 results -> storage type (round to nearest even; NaN stays NaN, overflow gives inf)
+template <typename T>
+__device__ __forceinline__ void store_quad(T* p, f32x4v v) {
+  if constexpr (sizeof(T) == 4) {
+    *reinterpret_cast<f32x4v*>(p) = v;
+  } else if constexpr (std::is_same<T, __half>::value) {
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    const h4 r = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
+    *reinterpret_cast<h4*>(p) = r;
+  } else {
+    typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+    const b4 r = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+    *reinterpret_cast<b4*>(p) = r;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ float ld1(const T* p) { return (float)*p; }
+template <typename T>
+__device__ __forceinline__ void st1(T* p, float v) { *p = (T)v; }
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
@@ -123,9 +163,9 @@ __device__ __forceinline__ float wave_max(float v) {
 // exponent e with x = f 2^e, f in [0.5, 1) (x > 0 finite)
 __device__ __forceinline__ int exp_of(float x) { return __builtin_amdgcn_frexp_expf(x); }
 
-template <int TMAX, bool MEAN>
+template <typename T, int TMAX, bool MEAN>
 __global__ __launch_bounds__(kThreads, 2) void ip_band_h2(
-    const float* __restrict__ L, const float* __restrict__ R, float* __restrict__ out, int C,
+    const T* __restrict__ L, const T* __restrict__ R, T* __restrict__ out, int C,
     int H, int W, int D, Strides4 ls, Strides4 rs, int tiles, int npass, int pw, int nwork) {
   using G = Geo<TMAX>;
   constexpr int DMAX = G::DMAX;
@@ -157,8 +197,9 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_h2(
   const int64_t cs = isR ? rs.c : ls.c;
   const bool cfull = C % kKC == 0;
 
+  using QT = typename Quad<T>::type;
   struct Set {
-    float4 v[8];
+    QT v[8];
     int nv;  // valid channels of v (0: pixels outside the image or an idle lane)
   };
   Set st;  // one set: the loads of step s+1 fly during step s's matrix work
@@ -169,17 +210,17 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_h2(
     const Work k = decode(wbeg + gi + it * gsz, tiles, npass, H, D, pw, DMAX);
     const int px = isR ? k.js + 4 * g : k.x0 + 4 * g - G::RW;
     const bool okp = active && px >= 0 && px < W;
-    const float* row = isR ? R + (int64_t)k.n * rs.n + (int64_t)k.y * rs.h
-                           : L + (int64_t)k.n * ls.n + (int64_t)k.y * ls.h;
-    const float* p = row + (okp ? px : 0) + (int64_t)min(c0, C - 1) * cs;
+    const T* row = isR ? R + (int64_t)k.n * rs.n + (int64_t)k.y * rs.h
+                       : L + (int64_t)k.n * ls.n + (int64_t)k.y * ls.h;
+    const T* p = row + (okp ? px : 0) + (int64_t)min(c0, C - 1) * cs;
     st.nv = okp ? min(max(C - c0, 0), 8) : 0;
     if (cfull) {
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk) st.v[kk] = *reinterpret_cast<const float4*>(p + kk * cs);
+      for (int kk = 0; kk < 8; ++kk) st.v[kk] = *reinterpret_cast<const QT*>(p + kk * cs);
     } else {
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk)
-        st.v[kk] = *reinterpret_cast<const float4*>(p + min(kk, max(C - 1 - c0, 0)) * cs);
+        st.v[kk] = *reinterpret_cast<const QT*>(p + min(kk, max(C - 1 - c0, 0)) * cs);
     }
   };
 
@@ -188,22 +229,25 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_h2(
   // split one step into the h / m planes (scaled by 2^k when k != 0)
   auto put = [&](Set& st) {
     if (!active) return;
+    float4 v[8];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) v[kk] = quad_to_f32<T>(st.v[kk]);
     if (__any(st.nv != 8)) {  // row edges / channel tail only
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk)
-        if (kk >= st.nv) st.v[kk] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (kk >= st.nv) v[kk] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk)
-      mx = fmaxf(mx, fmaxf(fmaxf(fabsf(st.v[kk].x), fabsf(st.v[kk].y)),
-                           fmaxf(fabsf(st.v[kk].z), fabsf(st.v[kk].w))));
+      mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v[kk].x), fabsf(v[kk].y)),
+                           fmaxf(fabsf(v[kk].z), fabsf(v[kk].w))));
     float col[4][8];
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
-      col[0][kk] = st.v[kk].x;
-      col[1][kk] = st.v[kk].y;
-      col[2][kk] = st.v[kk].z;
-      col[3][kk] = st.v[kk].w;
+      col[0][kk] = v[kk].x;
+      col[1][kk] = v[kk].y;
+      col[2][kk] = v[kk].z;
+      col[3][kk] = v[kk].w;
     }
     unsigned char* base = smem;
     auto split = [&](float sc, auto scaled) {
@@ -288,7 +332,7 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_h2(
   auto epilogue = [&](const Work& k) {
     const bool fullx = k.x0 + kXT <= W;
     const bool xlt = k.js < 0;  // some cells have x < d (their R rows are zero padding)
-    float* const olane = out + ((size_t)k.n * D + k.dp + srow) * plane_stride +
+    T* const olane = out + ((size_t)k.n * D + k.dp + srow) * plane_stride +
                          (size_t)k.y * W + k.x0 + 4 * lr;
     const bool okx = k.x0 + 4 * lr < W;
     const float mul = MEAN ? 1.0f / (float)C : 1.0f;
@@ -324,13 +368,13 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_h2(
         f32x4v v[4];
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) v[qq] = lds_load4(rb + 1024u * qq);
-        float* ol = olane + (size_t)(32 * a) * plane_stride;
+        T* ol = olane + (size_t)(32 * a) * plane_stride;
         asm volatile("" : "+v"(ol));
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
           const int dl = 32 * a + 2 * qq + srow;
           if (dl < k.Dp && (fullx || okx) && !(SMCV_ABLATE & 4))
-            *reinterpret_cast<f32x4v*>(ol + (size_t)(2 * qq) * plane_stride) = v[qq];
+            store_quad<T>(ol + (size_t)(2 * qq) * plane_stride, v[qq]);
         }
       }
     }
@@ -339,18 +383,18 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_h2(
   // exact fp32 path for a segment holding +-inf (or a scale fp32 cannot reach)
   auto slow_segment = [&](const Work& k) {
     const float mul = MEAN ? 1.0f / (float)C : 1.0f;
-    const float* lrow = L + (int64_t)k.n * ls.n + (int64_t)k.y * ls.h;
-    const float* rrow = R + (int64_t)k.n * rs.n + (int64_t)k.y * rs.h;
+    const T* lrow = L + (int64_t)k.n * ls.n + (int64_t)k.y * ls.h;
+    const T* rrow = R + (int64_t)k.n * rs.n + (int64_t)k.y * rs.h;
     for (int idx = tid; idx < k.Dp * kXT; idx += kThreads) {
       const int dl = idx / kXT, x = k.x0 + idx % kXT, d = k.dp + dl;
       if (x >= W) continue;
       float s = 0.f;
       if (x >= d) {
-        for (int c = 0; c < C; ++c) s = __builtin_fmaf(lrow[(int64_t)c * ls.c + x],
-                                                       rrow[(int64_t)c * rs.c + x - d], s);
+        for (int c = 0; c < C; ++c) s = __builtin_fmaf(ld1(lrow + (int64_t)c * ls.c + x),
+                                                       ld1(rrow + (int64_t)c * rs.c + x - d), s);
         s *= mul;
       }
-      out[(((size_t)k.n * D + d) * H + k.y) * W + x] = s;
+      st1(out + (((size_t)k.n * D + d) * H + k.y) * W + x, s);
     }
   };
 
@@ -444,15 +488,15 @@ int device_cus() {
   return cached[dev];
 }
 
-template <int TMAX>
-int launch(const float* l, const float* r, float* o, int64_t N, int64_t C, int64_t H, int64_t W,
+template <typename T, int TMAX>
+int launch(const T* l, const T* r, T* o, int64_t N, int64_t C, int64_t H, int64_t W,
            int64_t D, int64_t npass, int64_t pw, Strides4 ls, Strides4 rs, bool mean,
            hipStream_t st) {
   using G = Geo<TMAX>;
   const int tiles = (int)ceil_div(W, kXT);
   const int64_t nwork = (int64_t)tiles * H * N * npass;
   if (nwork > INT32_MAX / 64) return fail(SM_EINVAL, "inner product: too much work for one launch");
-  auto kern = mean ? ip_band_h2<TMAX, true> : ip_band_h2<TMAX, false>;
+  auto kern = mean ? ip_band_h2<T, TMAX, true> : ip_band_h2<T, TMAX, false>;
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::SHM);
   if (e != hipSuccess)
@@ -470,36 +514,41 @@ int check_dot_args(const void* left, const void* right, const void* out, int dty
                    int64_t C, int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
                    const int64_t* r_strides, Strides4* ls, Strides4* rs);
 
-// fp32 two-plane fp16 band kernel; *handled = false when the shape needs the generic path
-// (16-B pixel groups: W % 4 == 0, 4-float-aligned rows, C > 0).
+// Two-plane fp16 band kernel for fp32 / fp16 / bf16 features; *handled = false when the shape
+// needs the generic path (4-pixel groups: W % 4 == 0, 4-element aligned rows and base
+// pointers, C > 0).
 int band_h2_entry(const void* left, const void* right, void* out, int dtype, int64_t N, int64_t C,
                   int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
                   const int64_t* r_strides, int mode, void* stream, bool* handled) {
   *handled = false;
-  if (dtype != SM_F32) return SM_OK;
   Strides4 ls, rs;
   int rc = check_dot_args(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, &ls, &rs);
   if (rc) return rc;
+  const uintptr_t align = 4 * (uintptr_t)elem_size(dtype);
   const bool vec = (W % 4 == 0) && W >= 4 && C > 0 && ls.n % 4 == 0 && ls.c % 4 == 0 &&
                    ls.h % 4 == 0 && rs.n % 4 == 0 && rs.c % 4 == 0 && rs.h % 4 == 0 &&
-                   ((reinterpret_cast<uintptr_t>(left) | reinterpret_cast<uintptr_t>(right)) % 16 == 0);
+                   ((reinterpret_cast<uintptr_t>(left) | reinterpret_cast<uintptr_t>(right)) % align == 0);
   if (!vec) return SM_OK;
   *handled = true;
   if (N == 0 || H == 0 || D == 0) return SM_OK;
   const bool mean = mode == 1;
   hipStream_t st = as_stream(stream);
-  const float* l = static_cast<const float*>(left);
-  const float* r = static_cast<const float*>(right);
-  float* o = static_cast<float*>(out);
   using namespace h2band;
   // D passes of at most 192 disparities, balanced (D = 256: two passes of 128); a pass width
-  // that is a multiple of 4 keeps every right-window pixel group 16-B aligned
+  // that is a multiple of 4 keeps every right-window pixel group aligned
   const int64_t npass = ceil_div(D, (int64_t)192);
   const int64_t pw = (ceil_div(D, npass) + 3) / 4 * 4;
-  if (pw <= 32) return launch<2>(l, r, o, N, C, H, W, D, npass, pw, ls, rs, mean, st);
-  if (pw <= 64) return launch<3>(l, r, o, N, C, H, W, D, npass, pw, ls, rs, mean, st);
-  if (pw <= 128) return launch<5>(l, r, o, N, C, H, W, D, npass, pw, ls, rs, mean, st);
-  return launch<7>(l, r, o, N, C, H, W, D, npass, pw, ls, rs, mean, st);
+  SM_DISPATCH_DTYPE(dtype, T0, {
+    using T = typename std::conditional<std::is_same<T0, bf16_t>::value, __bf16, T0>::type;
+    const T* l = static_cast<const T*>(left);
+    const T* r = static_cast<const T*>(right);
+    T* o = static_cast<T*>(out);
+    if (pw <= 32) return launch<T, 2>(l, r, o, N, C, H, W, D, npass, pw, ls, rs, mean, st);
+    if (pw <= 64) return launch<T, 3>(l, r, o, N, C, H, W, D, npass, pw, ls, rs, mean, st);
+    if (pw <= 128) return launch<T, 5>(l, r, o, N, C, H, W, D, npass, pw, ls, rs, mean, st);
+    return launch<T, 7>(l, r, o, N, C, H, W, D, npass, pw, ls, rs, mean, st);
+  });
+  return SM_OK;
 }
 
 }  // namespace smcv

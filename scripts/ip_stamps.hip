@@ -6,7 +6,6 @@
 #include "../realtime_stereo_matcher_amd/csrc/cv_dot.hip"
 #include "../realtime_stereo_matcher_amd/csrc/ip_mfma.hip"
 #include "../realtime_stereo_matcher_amd/csrc/ip_f32.hip"
-#include "../realtime_stereo_matcher_amd/csrc/ip_ws.hip"
 #include "../realtime_stereo_matcher_amd/csrc/ip_h2.hip"
 
 namespace smcv {
@@ -25,12 +24,10 @@ int main(int argc, char** argv) {
   hipMalloc(&R, nin * 4);
   hipMalloc(&O, nout * 4);
   const bool f32 = argc > 2 && !strcmp(argv[2], "f32");
-  const bool ws = argc > 2 && !strcmp(argv[2], "ws");
   const bool h2 = argc > 2 && !strcmp(argv[2], "h2");
   bool handled = false;
   auto run = [&]() {
     if (h2) return smcv::band_h2_entry(L, R, O, SM_F32, N, C, H, W, D, nullptr, nullptr, 0, nullptr, &handled);
-    if (ws) return smcv::band_ws_entry(L, R, O, SM_F32, N, C, H, W, D, nullptr, nullptr, 0, nullptr, &handled);
     if (f32) return smcv::band_f32_entry(L, R, O, SM_F32, N, C, H, W, D, nullptr, nullptr, 0, nullptr, &handled);
     return smcv::band_mfma_entry(L, R, O, SM_F32, N, C, H, W, D, nullptr, nullptr, 0, nullptr);
   };
@@ -75,30 +72,6 @@ int main(int argc, char** argv) {
     printf("kernel h2 %.1f us rc=%d, waves: %d, %.0f cycles/wave\n", ms * 1e3, rc, n, tt / (n ? n : 1));
     for (int p = 0; p < 12; ++p)
       if (sm[p] > 0) printf("  %-30s %10.0f cycles/wave  %5.1f %%\n", hn[p], sm[p] / n, 100.0 * sm[p] / tt);
-    return 0;
-  }
-  if (ws) {
-    const char* wn[12] = {"math: barrier wait", "math: frags+mfma", "math: epi shear", "math: epi ring->store",
-                          "stage: split+lds write", "stage: load issue", "stage: barrier wait",
-                          "-", "-", "-", "-", "-"};
-    for (int role = 0; role < 2; ++role) {
-      double sm[12] = {0};
-      int n = 0;
-      for (int w = 0; w < 4096; ++w) {
-        if (((w & 7) < 4) != (role == 0)) continue;
-        unsigned long long t = 0;
-        for (int p = 0; p < 12; ++p) t += st[w][p];
-        if (!t) continue;
-        ++n;
-        for (int p = 0; p < 12; ++p) sm[p] += st[w][p];
-      }
-      double tt = 0;
-      for (int p = 0; p < 12; ++p) tt += sm[p];
-      printf("kernel ws %.1f us rc=%d, %s waves: %d, %.0f cycles/wave\n", ms * 1e3, rc,
-             role ? "stage" : "math", n, tt / (n ? n : 1));
-      for (int p = 0; p < 12; ++p)
-        if (sm[p] > 0) printf("  %-26s %10.0f cycles/wave  %5.1f %%\n", wn[p], sm[p] / n, 100.0 * sm[p] / tt);
-    }
     return 0;
   }
   printf("kernel: %s\n", f32 ? "f32 band" : "bf16x3 band");

@@ -19,7 +19,7 @@ def feats(shape, dtype):
 
 OPS = {
     "inner_product_mfma_cfg2": lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="mfma"))(*feats((1, 64, 540, 960), torch.float32)),
-    "inner_product_ws_cfg2": lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="ws"))(*feats((1, 64, 540, 960), torch.float32)),
+    "inner_product_h2_cfg2": lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="h2"))(*feats((1, 64, 540, 960), torch.float32)),
     "inner_product_bf16x3_cfg2": lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="bf16x3"))(*feats((1, 64, 540, 960), torch.float32)),
     "inner_product_valu_cfg2": lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="valu"))(*feats((1, 64, 540, 960), torch.float32)),
     "soft_argmin_cfg2": lambda: (lambda v: lambda: F.soft_argmin(v))(torch.randn(1, 192, 540, 960, device="cuda")),
