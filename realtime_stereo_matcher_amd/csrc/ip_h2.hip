@@ -40,8 +40,8 @@
 #include <type_traits>
 
 #ifndef SMCV_ABLATE
-#define SMCV_ABLATE 0  // diagnostics only (scripts/ip_stamps.hip): 1 no MFMA, 4 no stores
-#endif
+#define SMCV_ABLATE 0  // diagnostics only (scripts/ip_stamps.hip): 1 no MFMA, 2 all feature
+#endif                 // loads from one line, 4 no stores, 8 no epilogue
 
 namespace smcv {
 namespace h2band {
@@ -117,35 +117,72 @@ __device__ __forceinline__ __attribute__((address_space(3))) unsigned* lds_word(
 }
 
 // a 4-pixel group of one channel row in registers: 16 B (fp32) or 8 B (fp16 / bf16)
-template <typename T> struct Quad { using type = uint2; };
-template <> struct Quad<float> { using type = float4; };
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+template <typename T> struct Quad { using type = u32x2; };
+template <> struct Quad<float> { using type = f32x4v; };
+
+// Feature loads are issued by inline asm so that the compiler neither waits for them itself
+// (its control-flow merges would put vmcnt(0) -- a wait for every output store in flight --
+// in front of every step) nor knows them: the kernel counts vmcnt by hand (vm_wait).
+template <typename QT>
+__device__ __forceinline__ void gload(QT& v, const void* p) {
+  if constexpr (sizeof(QT) == 16) {
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  } else {
+    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  }
+}
+// Wait for the feature loads: vmcnt(N) when N output stores were issued after them (they may
+// stay in flight), else vmcnt(0).  One asm statement with the scalar branch inside, and the
+// loaded registers as tied operands: no use of them is scheduled before the wait, and the
+// register allocator has a single place (the load's destination) to keep them.
+template <int N, typename QT>
+__device__ __forceinline__ void vm_wait(QT (&v)[8], int after_stores) {
+  asm volatile(
+      "s_cmp_eq_u32 %8, 0\n\t"
+      "s_cbranch_scc1 .Lvm_all%=\n\t"
+      "s_waitcnt vmcnt(%9)\n\t"
+      "s_branch .Lvm_done%=\n"
+      ".Lvm_all%=:\n\t"
+      "s_waitcnt vmcnt(0)\n"
+      ".Lvm_done%=:"
+      : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
+        "+v"(v[7])
+      : "s"(after_stores), "n"(N)
+      : "memory", "scc");
+}
 
 template <typename T>
 __device__ __forceinline__ float4 quad_to_f32(typename Quad<T>::type q) {
   if constexpr (sizeof(T) == 4) {
-    return q;
+    return make_float4(q.x, q.y, q.z, q.w);
   } else if constexpr (std::is_same<T, __half>::value) {
-    const hp2 a = __builtin_bit_cast(hp2, q.x), b = __builtin_bit_cast(hp2, q.y);
-    return make_float4((float)a[0], (float)a[1], (float)b[0], (float)b[1]);
+    // (a bit_cast of q.y to a 2 x __fp16 vector miscompiles to q.x with ROCm 7.2 clang)
+    const unsigned x = q.x, y = q.y;
+    auto f = [](unsigned short b) { return (float)__builtin_bit_cast(_Float16, b); };
+    return make_float4(f(x & 0xffffu), f(x >> 16), f(y & 0xffffu), f(y >> 16));
   } else {  // bf16: the value is the high half of an fp32
     return make_float4(__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u),
                        __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u));
   }
 }
 
-// 4 fp32 results -> storage type (round to nearest even; NaN stays NaN, overflow gives inf)
+// 4 fp32 results -> storage type (round to nearest even; NaN stays NaN, overflow gives inf).
+// Global address space explicitly: a flat store would count in vmcnt out of order.
 template <typename T>
 __device__ __forceinline__ void store_quad(T* p, f32x4v v) {
+  typedef __attribute__((address_space(1))) void gvoid;
+  gvoid* g = (gvoid*)p;
   if constexpr (sizeof(T) == 4) {
-    *reinterpret_cast<f32x4v*>(p) = v;
+    *reinterpret_cast<__attribute__((address_space(1))) f32x4v*>(g) = v;
   } else if constexpr (std::is_same<T, __half>::value) {
     typedef _Float16 h4 __attribute__((ext_vector_type(4)));
     const h4 r = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
-    *reinterpret_cast<h4*>(p) = r;
+    *reinterpret_cast<__attribute__((address_space(1))) h4*>(g) = r;
   } else {
     typedef __bf16 b4 __attribute__((ext_vector_type(4)));
     const b4 r = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
-    *reinterpret_cast<b4*>(p) = r;
+    *reinterpret_cast<__attribute__((address_space(1))) b4*>(g) = r;
   }
 }
 
@@ -166,7 +203,8 @@ __device__ __forceinline__ int exp_of(float x) { return __builtin_amdgcn_frexp_e
 template <typename T, int TMAX, bool MEAN>
 __global__ __launch_bounds__(kThreads, 2) void ip_band_h2(
     const T* __restrict__ L, const T* __restrict__ R, T* __restrict__ out, int C,
-    int H, int W, int D, Strides4 ls, Strides4 rs, int tiles, int npass, int pw, int nwork) {
+    int H, int W, int D, Strides4 ls, Strides4 rs, int tiles, int npass, int pw, int nwork,
+    int stagger) {
   using G = Geo<TMAX>;
   constexpr int DMAX = G::DMAX;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -183,6 +221,10 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_h2(
   const int nitems = (wend - (wbeg + gi) + gsz - 1) / gsz;
   const int nks = (C + kKC - 1) / kKC;
   const int S = nitems * nks;  // pipeline steps of this workgroup
+  // the second workgroup of a CU starts later, so the two are not in phase (one streams its
+  // output while the other loads and multiplies)
+  if (stagger > 0 && blockIdx.x >= gridDim.x / 2)
+    for (int i = 0; i < stagger; ++i) __builtin_amdgcn_s_sleep(64);
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -195,7 +237,7 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_h2(
   const int g = min(tid - ch * G::GROUPS, G::GROUPS - 1);  // rows 4g .. 4g+3
   const bool isR = 4 * g < G::RW;
   const int64_t cs = isR ? rs.c : ls.c;
-  const bool cfull = C % kKC == 0;
+  const bool cfull = __builtin_amdgcn_readfirstlane(C % kKC) == 0;  // uniform: a scalar branch
 
   using QT = typename Quad<T>::type;
   struct Set {
@@ -213,15 +255,12 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_h2(
     const T* row = isR ? R + (int64_t)k.n * rs.n + (int64_t)k.y * rs.h
                        : L + (int64_t)k.n * ls.n + (int64_t)k.y * ls.h;
     const T* p = row + (okp ? px : 0) + (int64_t)min(c0, C - 1) * cs;
+    if (SMCV_ABLATE & 2) p = L + 4 * (lane & 7);
     st.nv = okp ? min(max(C - c0, 0), 8) : 0;
-    if (cfull) {
+    // channel tail: clamp to the last channel (one code path; put() zeroes the tail)
+    const int lim = cfull ? 7 : min(max(C - 1 - c0, 0), 7);
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk) st.v[kk] = *reinterpret_cast<const QT*>(p + kk * cs);
-    } else {
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk)
-        st.v[kk] = *reinterpret_cast<const QT*>(p + min(kk, max(C - 1 - c0, 0)) * cs);
-    }
+    for (int kk = 0; kk < 8; ++kk) gload(st.v[kk], p + min(kk, lim) * cs);
   };
 
   int kL = 0, kR = 0;  // per-segment scale exponents (workgroup-uniform)
@@ -273,7 +312,7 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_h2(
         *reinterpret_cast<uint4*>(base + G::PLANE + off) = wm;
       }
     };
-    if ((kL | kR) == 0) {
+    if (__builtin_amdgcn_readfirstlane(kL | kR) == 0) {  // uniform: a scalar branch
       split(1.0f, std::false_type{});
     } else {
       split(__builtin_ldexpf(1.0f, isR ? kR : kL), std::true_type{});
@@ -329,14 +368,16 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_h2(
   const unsigned rbase = ring0 + (unsigned)srow * 512u + 16u * lr;
   const size_t plane_stride = (size_t)H * W;
 
-  auto epilogue = [&](const Work& k) {
+  // SCALE: multiply back by 2^-(kL+kR); XLT: the segment has cells x < d (R pad rows), forced
+  // to 0 (an R pad row can meet a NaN).  Compile-time, so the common case costs no VALU.
+  auto epilogue_v = [&](const Work& k, bool fast, auto scale, auto xlt) {
     const bool fullx = k.x0 + kXT <= W;
-    const bool xlt = k.js < 0;  // some cells have x < d (their R rows are zero padding)
     T* const olane = out + ((size_t)k.n * D + k.dp + srow) * plane_stride +
                          (size_t)k.y * W + k.x0 + 4 * lr;
     const bool okx = k.x0 + 4 * lr < W;
     const float mul = MEAN ? 1.0f / (float)C : 1.0f;
     const int kk = -(kL + kR);
+    const int jlane = k.js + 32 * wave + 4 * hh;  // R row of element c_i of block 0, minus c_i
 #pragma unroll
     for (int t = TMAX - 1; t >= 0; --t) {
       const int a = TMAX - 2 - t;
@@ -348,11 +389,8 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_h2(
         const int ci = (i & 3) + 8 * (i >> 2);
         float val = acc[t][i];
         if (MEAN) val *= mul;
-        if (kk != 0) val = __builtin_ldexpf(val, kk);
-        if (xlt) {  // x < d: the reference writes 0 (an R pad row can meet a NaN / inf)
-          const int j = k.js + 32 * (wave + t) + ci + 4 * hh;
-          val = j >= 0 ? val : 0.f;
-        }
+        if constexpr (decltype(scale)::value) val = __builtin_ldexpf(val, kk);
+        if constexpr (decltype(xlt)::value) val = jlane + 32 * t + ci >= 0 ? val : 0.f;
         unsigned addr;
         if (sa != 2) {  // ring0 + col + slot(a+1) kSlot + (u - c_i) 512, both cases
           addr = wb + (unsigned)(sb * kSlot - ci * 512);
@@ -370,13 +408,32 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_h2(
         for (int qq = 0; qq < 4; ++qq) v[qq] = lds_load4(rb + 1024u * qq);
         T* ol = olane + (size_t)(32 * a) * plane_stride;
         asm volatile("" : "+v"(ol));
+        if (fast) {  // every store valid: exactly 4 (T-1) per lane, counted by vm_wait
 #pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-          const int dl = 32 * a + 2 * qq + srow;
-          if (dl < k.Dp && (fullx || okx) && !(SMCV_ABLATE & 4))
-            store_quad<T>(ol + (size_t)(2 * qq) * plane_stride, v[qq]);
+          for (int qq = 0; qq < 4; ++qq) store_quad<T>(ol + (size_t)(2 * qq) * plane_stride, v[qq]);
+        } else {
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            const int dl = 32 * a + 2 * qq + srow;
+            if (dl < k.Dp && (fullx || okx) && !(SMCV_ABLATE & 4))
+              store_quad<T>(ol + (size_t)(2 * qq) * plane_stride, v[qq]);
+          }
         }
       }
+    }
+  };
+
+  auto epilogue = [&](const Work& k, bool fast) {
+    using TT = std::true_type;
+    using FF = std::false_type;
+    const bool sc = __builtin_amdgcn_readfirstlane(kL + kR) != 0;
+    const bool xl = __builtin_amdgcn_readfirstlane(k.js) < 0;
+    if (sc) {
+      if (xl) epilogue_v(k, fast, TT{}, TT{});
+      else epilogue_v(k, fast, TT{}, FF{});
+    } else {
+      if (xl) epilogue_v(k, fast, FF{}, TT{});
+      else epilogue_v(k, fast, FF{}, FF{});
     }
   };
 
@@ -403,6 +460,7 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_h2(
   const unsigned maxw = lds_addr(smem + G::MAXW);
   if (tid < 4) *reinterpret_cast<__attribute__((address_space(3))) unsigned*>(maxw + 4 * tid) = 0u;
   bool redone = false;  // the current segment is a recomputation
+  bool pend = false;    // 4 (T-1) output stores were issued after the outstanding feature loads
   // one pipeline step; returns true when the segment must be recomputed from its first step
   auto body = [&](int s) -> bool {
     const int it = s / nks;
@@ -411,6 +469,8 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_h2(
     if (ks == 0) mx = 0.f;
     __syncthreads();  // A: the previous step's fragment reads are done
     SM_STAMP(0);
+    vm_wait<4 * (TMAX - 1)>(st.v, __builtin_amdgcn_readfirstlane((int)pend));
+    pend = false;
     put(st);
     const unsigned par = (unsigned)(it & 1) * 8u;
     if (ks == nks - 1) {
@@ -443,7 +503,9 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_h2(
     const bool okl = ml == 0.f || (el + kL <= 15 && el + kL >= -1);
     const bool okr = mr == 0.f || (er + kR <= 15 && er + kR >= -1);
     if (fin && okl && okr) {
-      epilogue(k);
+      const bool fast = k.x0 + kXT <= W && k.Dp == DMAX && !(SMCV_ABLATE & 12);
+      if (!(SMCV_ABLATE & 8)) epilogue(k, fast);
+      pend = fast;  // exactly 4 (T-1) stores per lane were issued after the loads
       SM_STAMP(4);
       redone = false;
       return false;
@@ -466,11 +528,13 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_h2(
   load(st, 0);
   for (int s = 0; s < S; ++s) {
     if (body(s)) {  // recompute the segment: restart its steps
+      vm_wait<0>(st.v, 0);  // the registers must not have a load in flight when reloaded
       s = (s / nks) * nks;
       load(st, s);
       --s;
     }
   }
+  vm_wait<0>(st.v, 0);  // the last (clamped) prefetch lands before its registers die
   SM_STAMP_FLUSH
 }
 
@@ -486,6 +550,17 @@ int device_cus() {
     cached[dev] = n;
   }
   return cached[dev];
+}
+
+// start offset of the second workgroup per CU, in units of 64 x 64 cycles (diagnostic override:
+// STEREOCV_H2_STAGGER)
+int stagger_units() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("STEREOCV_H2_STAGGER");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
 }
 
 template <typename T, int TMAX>
@@ -504,7 +579,8 @@ int launch(const T* l, const T* r, T* o, int64_t N, int64_t C, int64_t H, int64_
   int64_t nwg = std::min<int64_t>(nwork, 2 * (int64_t)device_cus());
   nwg = std::max<int64_t>(8, (nwg + 7) / 8 * 8);
   hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(kThreads), G::SHM, st, l, r, o, (int)C,
-                     (int)H, (int)W, (int)D, ls, rs, tiles, (int)npass, (int)pw, (int)nwork);
+                     (int)H, (int)W, (int)D, ls, rs, tiles, (int)npass, (int)pw, (int)nwork,
+                     stagger_units());
   return check_launch("ip_band_h2");
 }
 
