@@ -8,7 +8,14 @@ disparity regression (model/mobile_disp_net_c.py:208-220).  A STEP is one pass o
 path over the rank's batch of pairs (inputs already resident in HBM), plus -- for N>1 -- the
 RCCL gather of the per-pair disparities to rank 0 (the only collective).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--algo auto|bf16x3|f32|valu]
+Pipelines (--pipeline):
+  separate        (default) the volume kernel (--algo), then the regression kernel reading the
+                  (N,D,H,W) volume back -- the reference's two calls;
+  fused           one band-kernel launch writes the volume AND its soft-argmin
+                  (functional.inner_product_soft_argmin);
+  fused-novolume  SURVEY §8f-1: the same kernel without writing the volume.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--pipeline P] [--algo A]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
 Rank 0 prints ONE JSON line.  ``value`` = pairs processed by all ranks / max-over-ranks wall
@@ -36,9 +43,15 @@ C, H, W, D = 64, 540, 960, 192
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
 
-def cv_algorithmic_bytes(batch):
-    # read L + read R + write the (N, D, H, W) fp32 volume once
-    return batch * (2 * C * H * W + D * H * W) * 4
+def kernel_algorithmic_bytes(batch, pipeline):
+    """Algorithmic bytes of the timed (dominant) kernel per launch: read L + R,
+    write the (N, D, H, W) fp32 volume once; the fused kernel also writes the disparities."""
+    feats, vol, disp = 2 * C * H * W * 4, D * H * W * 4, H * W * 4
+    if pipeline == "separate":
+        return batch * (feats + vol)
+    if pipeline == "fused":
+        return batch * (feats + vol + disp)
+    return batch * (feats + disp)
 
 
 def parse():
@@ -47,7 +60,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=1, help="stereo pairs per GPU per step")
-    ap.add_argument("--algo", default="auto", choices=["auto", "h2", "bf16x3", "f32", "mfma", "valu"])
+    ap.add_argument("--algo", default="auto", choices=["auto", "h2", "bf16x3", "f32", "mfma", "valu"],
+                    help="volume kernel of --pipeline separate")
+    ap.add_argument("--pipeline", default="separate", choices=["separate", "fused", "fused-novolume"])
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
                     help="bounded CPU-baseline sample length (0 disables)")
     return ap.parse_args()
@@ -114,15 +129,24 @@ def main():
 
     ev = []  # (start, end) around the CV kernel, timed steps only
 
+    if a.pipeline != "separate" and a.algo not in ("auto", "h2"):
+        raise SystemExit("--algo selects the volume kernel of --pipeline separate")
+
     def step(timed):
         if timed:
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
-        vol = F.inner_product_volume(L, R, D, algo=a.algo)
+        if a.pipeline == "separate":
+            vol = F.inner_product_volume(L, R, D, algo=a.algo)
+            if timed:
+                e.record()
+            disp = F.soft_argmin(vol)  # (B, 1, H, W)
+        else:
+            _, disp = F.inner_product_soft_argmin(L, R, D, keep_volume=a.pipeline == "fused")
+            if timed:
+                e.record()
         if timed:
-            e.record()
             ev.append((s, e))
-        disp = F.soft_argmin(vol)  # (B, 1, H, W)
         return gather_disparities(disp, global_batch)
 
     for _ in range(a.warmup):
@@ -144,9 +168,12 @@ def main():
         elapsed = float(t.item())
 
     cv_ms = sum(s.elapsed_time(e) for s, e in ev) / max(1, len(ev))
-    achieved = cv_algorithmic_bytes(B) / (cv_ms * 1e-3) / 1e9
-    kname = {"valu": "dot_volume_valu", "f32": "ip_band_f32", "mfma": "ip_band_f32",
-             "bf16x3": "ip_band_mfma"}.get(a.algo, "ip_band_h2")
+    nbytes = kernel_algorithmic_bytes(B, a.pipeline)
+    achieved = nbytes / (cv_ms * 1e-3) / 1e9
+    kname = "band_h2"
+    if a.pipeline == "separate":
+        kname = {"valu": "dot_volume_valu", "f32": "ip_band_f32", "mfma": "ip_band_f32",
+                 "bf16x3": "ip_band_mfma"}.get(a.algo, "band_h2")
     traffic = traffic_from_profiles(kname)
     pairs = global_batch * a.steps
     rec = {
@@ -166,11 +193,11 @@ def main():
         "config": {"workload": "BASELINE configs[1]: mobile_stereo_net inner_product CV, 1/4-res KITTI "
                                "540x960, C=64, D=192, fp32 + soft-argmin regression",
                    "C": C, "H": H, "W": W, "D": D, "batch_per_gpu": B, "global_batch": global_batch,
-                   "parallelism": f"dp{world}", "algo": a.algo},
+                   "parallelism": f"dp{world}", "algo": a.algo, "pipeline": a.pipeline},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": kname, "avg_kernel_us": cv_ms * 1e3,
-                     "algorithmic_bytes_per_launch": cv_algorithmic_bytes(B)},
+                     "algorithmic_bytes_per_launch": nbytes},
     }
     if rank == 0 and world == 1 and a.cpu_baseline_seconds > 0:
         rec["cpu_baseline"] = cpu_baseline(a.cpu_baseline_seconds)

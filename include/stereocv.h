@@ -28,7 +28,13 @@ extern "C" {
 #endif
 
 enum sm_dtype { SM_F32 = 0, SM_F16 = 1, SM_BF16 = 2 };
-enum sm_status { SM_OK = 0, SM_EINVAL = -1, SM_EDTYPE = -2, SM_ELAUNCH = -3 };
+enum sm_status {
+  SM_OK = 0,
+  SM_EINVAL = -1,
+  SM_EDTYPE = -2,
+  SM_ELAUNCH = -3,
+  SM_EUNSUPPORTED = -4 /* sm_cv_inner_product_softargmin without a volume: shape not fused */
+};
 enum sm_argext_mode { SM_ARGMIN = 0, SM_ARGMAX = 1 };
 enum sm_regress_flags {
   SM_REGRESS_SOFTMAX = 0,      /* softmax over D inside (mobile_disp_net_c.py:208-220) */
@@ -41,9 +47,10 @@ enum sm_ip_algo {
   SM_IP_MFMA_F32 = 2,    /* banded C-contraction on v_mfma_f32_16x16x4_f32 (exact fp32 fma) */
   SM_IP_MFMA_BF16X3 = 3, /* banded C-contraction on bf16 MFMA over an exact 3-way bf16 split */
   /* 4: reserved (a retired warp-specialised variant of the bf16 split) */
-  SM_IP_MFMA_H2 = 5      /* default: per-segment power-of-two scale + range-checked two-plane
-                            fp16 split on 32x32x16 f16 MFMA, two workgroups per CU; segments
-                            holding +-inf take an exact fp32 path (any input dtype) */
+  SM_IP_MFMA_H2 = 5      /* default: banded contraction on 32x32x16 MFMA, two workgroups per CU;
+                            fp16 / bf16 features as they are (exact products), fp32 features as
+                            a per-segment power-of-two scaled, range-checked two-plane fp16 split
+                            (segments holding +-inf take an exact fp32 path) */
 };
 
 /* Library version (major*10000 + minor*100 + patch). */
@@ -70,6 +77,22 @@ int sm_cv_inner_product_ex(const void* left, const void* right, void* out, int d
 int sm_cv_correlation_mean(const void* left, const void* right, void* out, int dtype,
                            int64_t N, int64_t C, int64_t H, int64_t W, int64_t D,
                            const int64_t* l_strides, const int64_t* r_strides, void* stream);
+
+/* f-1: cost volume + soft-argmin regression in one pass.
+ *   mode 0: TorchInnerProductCost -- cost_volume/inner_product.py:11-42; mode 1:
+ *   make_correlation_volume -- model/mobile_disp_net_c.py:188-205; each followed by
+ *   disparity_regression -- model/mobile_disp_net_c.py:208-220 (= the inline soft-argmin of
+ *   model/mobile_stereo_net.py:144-147).
+ * disparity[n,y,x] = sum_d d * softmax_d(vol[n,:,y,x]): (N, H, W) in `dtype`; the (N, D, H, W)
+ * volume is written too when out_volume != NULL.  fp32 features with W % 4 == 0, 16-B aligned
+ * rows and D <= 192 take the fused band kernel (the volume is never read back; with
+ * out_volume == NULL it is never written).  Other shapes run the volume and the regression as
+ * two kernels, which needs out_volume: with out_volume == NULL they return SM_EUNSUPPORTED.
+ * D == 0: the disparity is 0 (an empty softmax axis). */
+int sm_cv_inner_product_softargmin(const void* left, const void* right, void* out_volume,
+                                   void* disparity, int dtype, int64_t N, int64_t C, int64_t H,
+                                   int64_t W, int64_t D, const int64_t* l_strides,
+                                   const int64_t* r_strides, int mode, void* stream);
 
 /* a-2: TorchGroupwiseCost(n_groups, max_disparity)(left, right)
  *      -- cost_volume/groupwise.py:24-56

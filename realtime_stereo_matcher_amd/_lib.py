@@ -11,7 +11,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("STEREOCV_LIB", os.path.join(_HERE, "libstereocv.so"))
 
 SM_F32, SM_F16, SM_BF16 = 0, 1, 2
-SM_OK, SM_EINVAL, SM_EDTYPE, SM_ELAUNCH = 0, -1, -2, -3
+SM_OK, SM_EINVAL, SM_EDTYPE, SM_ELAUNCH, SM_EUNSUPPORTED = 0, -1, -2, -3, -4
 SM_ARGMIN, SM_ARGMAX = 0, 1
 SM_REGRESS_SOFTMAX, SM_REGRESS_PRESOFTMAXED = 0, 1
 SM_IP_AUTO, SM_IP_VALU, SM_IP_MFMA_F32, SM_IP_MFMA_BF16X3, SM_IP_MFMA_H2 = 0, 1, 2, 3, 5
@@ -29,6 +29,7 @@ SIGNATURES = {
     "sm_cv_inner_product_ex": [_p, _p, _p, _i, _l, _l, _l, _l, _l, _lp, _lp, _i, _p],
     "sm_cv_correlation_mean": [_p, _p, _p, _i, _l, _l, _l, _l, _l, _lp, _lp, _p],
     "sm_cv_groupwise": [_p, _p, _p, _i, _l, _l, _l, _l, _l, _l, _lp, _lp, _p],
+    "sm_cv_inner_product_softargmin": [_p, _p, _p, _p, _i, _l, _l, _l, _l, _l, _lp, _lp, _i, _p],
     "sm_cv_concat": [_p, _p, _p, _i, _l, _l, _l, _l, _l, _lp, _lp, _p],
     "sm_cv_interweave": [_p, _p, _p, _i, _l, _l, _l, _l, _lp, _lp, _p],
     "sm_cv_interweave_shifted": [_p, _p, _p, _i, _l, _l, _l, _l, _l, _lp, _lp, _p],

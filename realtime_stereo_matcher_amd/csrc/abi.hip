@@ -15,6 +15,14 @@ int band_f32_entry(const void* left, const void* right, void* out, int dtype, in
 int band_h2_entry(const void* left, const void* right, void* out, int dtype, int64_t N, int64_t C,
                   int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
                   const int64_t* r_strides, int mode, void* stream, bool* handled);
+int band_h2_groupwise_entry(const void* left, const void* right, float* out, int dtype, int64_t N,
+                            int64_t C, int64_t H, int64_t W, int64_t D, int64_t G,
+                            const int64_t* l_strides, const int64_t* r_strides, void* stream,
+                            bool* handled);
+int band_h2_fused_entry(const void* left, const void* right, void* out, float* disp, int dtype,
+                        int64_t N, int64_t C, int64_t H, int64_t W, int64_t D,
+                        const int64_t* l_strides, const int64_t* r_strides, int mode,
+                        void* stream, bool* handled);
 int ip_mfma_entry(const void* left, const void* right, void* out, int dtype, int64_t N,
                   int64_t C, int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
                   const int64_t* r_strides, void* stream, bool* handled);
@@ -98,8 +106,44 @@ extern "C" int sm_cv_groupwise(const void* left, const void* right, float* out, 
                                const int64_t* l_strides, const int64_t* r_strides,
                                void* stream) {
   SM_ENTRY_BEGIN
+  // the MFMA band kernel (D-innermost epilogue); shapes it does not take: the VALU kernel
+  bool handled = false;
+  int rc = band_h2_groupwise_entry(left, right, out, dtype, N, C, H, W, D, G, l_strides,
+                                   r_strides, stream, &handled);
+  if (handled || rc != SM_OK) return rc;
   return dot_volume_valu_entry(left, right, out, dtype, N, C, H, W, D, G, l_strides, r_strides,
                                2, stream);
+}
+
+extern "C" int sm_cv_inner_product_softargmin(const void* left, const void* right,
+                                              void* out_volume, void* disparity, int dtype,
+                                              int64_t N, int64_t C, int64_t H, int64_t W,
+                                              int64_t D, const int64_t* l_strides,
+                                              const int64_t* r_strides, int mode, void* stream) {
+  SM_ENTRY_BEGIN
+  if (mode != 0 && mode != 1) return fail(SM_EINVAL, "mode must be 0 (sum) or 1 (mean)");
+  if (!valid_dtype(dtype)) return fail(SM_EDTYPE, "unsupported dtype code");
+  if (D == 0 && N * H * W > 0) {  // softmax over an empty axis: the weighted sum is 0
+    if (disparity == nullptr) return fail(SM_EINVAL, "null disparity pointer");
+    const hipError_t e = hipMemsetAsync(disparity, 0, (size_t)(N * H * W) * elem_size(dtype),
+                                        as_stream(stream));
+    return e == hipSuccess ? SM_OK : fail(SM_ELAUNCH, hipGetErrorString(e));
+  }
+  bool handled = false;
+  int rc = band_h2_fused_entry(left, right, out_volume, static_cast<float*>(disparity), dtype, N,
+                               C, H, W, D, l_strides, r_strides, mode, stream, &handled);
+  if (handled || rc != SM_OK) return rc;
+  if (out_volume == nullptr)
+    return fail(SM_EUNSUPPORTED,
+                "fused cost volume + soft-argmin needs fp32 features, W % 4 == 0, 16-B aligned "
+                "rows and D <= 192; pass a volume buffer for the two-kernel path");
+  rc = mode == 1 ? sm_cv_correlation_mean(left, right, out_volume, dtype, N, C, H, W, D,
+                                          l_strides, r_strides, stream)
+                 : sm_cv_inner_product(left, right, out_volume, dtype, N, C, H, W, D, l_strides,
+                                       r_strides, stream);
+  if (rc != SM_OK) return rc;
+  return softargmin_entry(out_volume, disparity, dtype, N, D, H, W, SM_REGRESS_SOFTMAX, nullptr,
+                          stream);
 }
 
 extern "C" int sm_cv_concat(const void* left, const void* right, void* out, int dtype, int64_t N,

@@ -30,13 +30,11 @@ template <typename U> struct vec16 {
   U v[N];
 };
 
+// Plain 16-B stores: streaming whole 128-B lines they write at 5.8-6.2 TB/s, where the
+// non-temporal form reached 5.1 TB/s (store microbenchmark, r01).
 template <typename U>
 __device__ __forceinline__ void store16(U* dst, const vec16<U>& s) {
-  const uint4 q = *reinterpret_cast<const uint4*>(s.v);
-  __builtin_nontemporal_store(q.x, reinterpret_cast<uint32_t*>(dst) + 0);
-  __builtin_nontemporal_store(q.y, reinterpret_cast<uint32_t*>(dst) + 1);
-  __builtin_nontemporal_store(q.z, reinterpret_cast<uint32_t*>(dst) + 2);
-  __builtin_nontemporal_store(q.w, reinterpret_cast<uint32_t*>(dst) + 3);
+  *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(s.v);
 }
 
 // Stage left/right rows (n, c, y) into LDS as raw bits.

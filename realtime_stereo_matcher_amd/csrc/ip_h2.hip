@@ -1,63 +1,83 @@
-// Inner-product / correlation cost volume on gfx950 matrix cores, fp16 two-plane split
-// ("h2"): the fp32 default of sm_cv_inner_product / sm_cv_correlation_mean.
+// Band cost volumes on gfx950 matrix cores ("h2" kernels): inner product / correlation
+// (N, D, H, W), groupwise (N, G, H, W, D), and the inner product fused with soft-argmin.
 //
 // Reference: TorchInnerProductCost.forward  cost_volume/inner_product.py:11-42 (sum over C)
 //            make_correlation_volume         model/mobile_disp_net_c.py:188-205 (mean over C)
+//            TorchGroupwiseCost.forward      cost_volume/groupwise.py:24-56 (mean per group, D last)
+//            disparity_regression            model/mobile_disp_net_c.py:208-220 (fused variant)
 //   out[n, d, y, x] = sum_c L[n,c,y,x] * R[n,c,y,x-d]   (x >= d),   0 (x < d)
 //
 // Per image row the volume is a band of the contraction S[j][x] = sum_c R[c][j] L[c][x]
-// (d = x - j).  A workgroup (4 waves) owns a 128-pixel row segment; wave w owns x-block w
-// (32 pixels) and its T = 1 + DMAX/32 32x32 band blocks, accumulated with
-// v_mfma_f32_32x32x16_f16.  Every wave does everything (load, split, MFMA, shear, store) and
-// the CU holds TWO such workgroups, so one workgroup's output stream overlaps the other's
-// matrix work without any intra-workgroup role split.
+// (d = x - j).  A workgroup (4 waves) owns a 128-pixel row segment of one channel group; wave w
+// owns x-block w (32 pixels) and its T = 1 + DMAX/32 32x32 band blocks, accumulated on the
+// matrix cores.  Every wave does everything (load, stage, MFMA, shear, store) and the CU holds
+// TWO such workgroups, so one workgroup's output stream overlaps the other's loads and MFMAs.
 //
-// Arithmetic.  Each fp32 value is scaled by a per-segment power of two 2^k (exact) and split
-// into two fp16 planes by round-toward-zero: h = rtz16(x 2^k), m = rtz16(x 2^k - h).  Then
-// x 2^k = h + m + e with |e| < 2^-20 |x 2^k| (+ 2^-24 absolute below the fp16 normal range),
-// and the products h*h' + h*m' + m*h' (exact in fp32; the dropped m*m', h*e', e*h' are each
-// below 2^-20 relative) accumulate in fp32 on the matrix cores.  The result is multiplied back
-// by 2^-(kL+kR) (ldexp, exact).  Integer-valued features are exact (m = 0).
+// Operands.  fp16 / bf16 features are staged as they are (one plane; their products are exact
+// in fp32: one MFMA per block and 16-channel step).  fp32 features are scaled by a per-segment
+// power of two 2^k (exact) and split into two fp16 planes by round-toward-zero:
+// h = rtz16(x 2^k), m = rtz16(x 2^k - h), so x 2^k = h + m + e with |e| < 2^-20 |x 2^k|
+// (+ 2^-24 absolute below the fp16 normal range); the products h*h' + h*m' + m*h' (exact in
+// fp32; the dropped m*m', h*e', e*h' are each below 2^-20 relative) accumulate in fp32, and
+// the result is multiplied back by 2^-(kL+kR) (ldexp, exact).  Integer features are exact.
 //
-// Scale control (range safety of fp16).  Every lane tracks max|x| of the values it stages; at
-// the end of a segment the workgroup knows max|L| and max|R| over everything it staged.  The
-// segment is accepted when both scaled maxima lie in [2^-2, 2^15) (or are 0); otherwise the
-// segment is recomputed with k = 13 - exponent(max) (scaled maximum in [2^12, 2^13)), and that
-// k carries to the next segment, so smoothly varying feature scales cost nothing.  Segments
-// holding +-inf (or a scale fp32 cannot reach) take an exact fp32 FMA path.  NaN needs no
-// special case: it propagates through the split and the products like through the reference
-// sum, and cells x < d are forced to 0 as in the reference.
+// Scale control (fp32).  Every lane tracks max|x| of the values it stages; at the end of a
+// segment the workgroup knows max|L| and max|R| over everything it staged.  The segment is
+// accepted when both scaled maxima lie in [2^-2, 2^15) (or are 0); otherwise it is recomputed
+// with k = 13 - exponent(max) (scaled maximum in [2^12, 2^13)), and that k carries to the next
+// segment, so smoothly varying feature scales cost nothing.  Segments holding +-inf (or a scale
+// fp32 cannot reach) take an exact fp32 FMA path.  NaN needs no special case: it propagates
+// through the split and the products like through the reference sum.  Cells x < d are forced
+// to 0 as in the reference (an R pad row can meet a NaN or an inf).
 //
 // Data flow per 16-channel step (one barrier pair): the step's features were loaded into
-// registers one step earlier; barrier A (the previous step's fragment reads are done), split
-// into the two planes in LDS (row/chunk XOR swizzle: conflict-free 16-B writes and fragment
-// reads, scripts/check_swizzle.py), issue the loads of step s+1, barrier B, 3 MFMAs per band
-// block.  After a segment's last step the accumulators are sheared (d = x - j) block by block
-// through a 3-slot ring of 32-row x 512-B chunks; each block completes one chunk, which the
-// four waves stream out as 512-B row segments (two rows per store instruction).
+// registers one step earlier (inline-asm loads whose vmcnt is counted by hand, so the output
+// stores stay in flight: vm_wait), and their 128-B lines were touched into L2 one step before
+// that (touch); barrier A (the previous step's fragment reads are done), stage into the
+// plane(s) in LDS (row/chunk XOR swizzle: conflict-free 16-B writes and fragment reads,
+// scripts/check_swizzle.py), issue the loads of the next step and the touches of the one after,
+// barrier B, MFMAs.  After a segment's last step each wave shears its accumulators (d = x - j)
+// block by block through a private 3-slot ring of 32 x 32 chunks -- no barrier -- and streams
+// every completed chunk out: NDHW as 8 rows x 128 B per store instruction, NGHWD as 8 pixels x
+// 128 B of d.
+//
+// Fused soft-argmin (FUSE).  While a chunk is in registers for its stores, each lane folds its
+// 4 rows x 4 pixels into an online softmax (running max; sums of e and d*e per chunk in fp32
+// relative to the chunk's first row, across chunks in fp64); the 8 lanes of a pixel column
+// merge by cross-lane shuffles after the last chunk, so the segment's disparities leave the
+// same pass -- with or without the volume.
 #include "common.h"
+
+#include <math.h>
 
 #include <type_traits>
 
 #ifndef SMCV_ABLATE
 #define SMCV_ABLATE 0  // diagnostics only (scripts/ip_stamps.hip): 1 no MFMA, 2 all feature
 #endif                 // loads from one line, 4 no stores, 8 no epilogue
+#ifndef SMCV_PREFETCH
+#define SMCV_PREFETCH 0  // L2 touches two steps ahead (1: on; measured slower on cfg2, r01)
+#endif
 
 namespace smcv {
 namespace h2band {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __fp16 hp2 __attribute__((ext_vector_type(2)));
 typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kWaves = 4;
 constexpr int kThreads = 64 * kWaves;
 constexpr int kXT = 32 * kWaves;    // left pixels per row segment
 constexpr int kKC = 16;             // channels per step (one 32x32x16 k-step)
-constexpr int kRowB = 32;           // bytes per plane row: 16 fp16
-constexpr int kSlot = 32 * 512;     // one ring chunk: 32 output rows x 128 px fp32
-constexpr int kRing = 3 * kSlot;
+constexpr int kRowB = 32;           // bytes per plane row: 16 x 16-bit
+constexpr int kSlot = 32 * 32 * 4;  // one ring chunk: 32 x 32 fp32
+constexpr int kRingW = 3 * kSlot;   // a wave's ring
+constexpr int kPF = SMCV_PREFETCH ? 1 : 0;  // touch instructions issued after each step's loads
+enum { kNDHW = 0, kNGHWD = 1 };
 
 // byte offset of (plane row r, 8-channel chunk h).  Fragment reads: lane l -> row base + (l & 31),
 // chunk l >> 5; plane writes: 8 consecutive lanes -> rows 4i + p of one 32-row block.  Both are
@@ -66,38 +86,53 @@ __device__ __forceinline__ int swz(int r, int h) {
   return ((r ^ ((r >> 2) & 3)) << 5) + ((h ^ ((r >> 4) & 1)) << 4);
 }
 
-template <int TMAX>
+template <typename T, int TMAX>
 struct Geo {
+  static constexpr int NP = sizeof(T) == 4 ? 2 : 1;  // operand planes
   static constexpr int DMAX = 32 * (TMAX - 1);
   static constexpr int RW = kXT + DMAX;   // right-window rows
   static constexpr int ROWS = RW + kXT;   // + left-tile rows
   static constexpr int PLANE = ROWS * kRowB;
   static constexpr int GROUPS = ROWS / 4; // 4-pixel groups per 8-channel chunk
   static constexpr int ITEMS = 2 * GROUPS;
-  static constexpr int RING = 2 * PLANE;  // ring byte offset
-  static constexpr int MAXW = RING + kRing;  // 4 words: max|L|, max|R| for segment parity 0/1
+  static constexpr int RING = NP * PLANE;              // the four wave rings
+  static constexpr int MAXW = RING + kWaves * kRingW;  // max|L|, max|R| for segment parity 0/1
   static constexpr size_t SHM = (size_t)MAXW + 16;
   static_assert(ITEMS <= kThreads, "one staging item per lane");
   static_assert(GROUPS % 8 == 0, "8-lane write groups stay inside one chunk");
   static_assert(SHM * 2 <= 160 * 1024, "two workgroups per CU");
 };
 
-struct Work {
-  int n, y, x0, dp, Dp, js;
+struct Args {
+  const void* L;
+  const void* R;
+  void* out;    // volume; nullptr: not stored (fused kernel only)
+  float* disp;  // fused kernel: (N, H, W) disparities
+  int C, cpg, G, H, W, D;
+  Strides4 ls, rs;
+  int tiles, npass, pw, nwork;
+  float mul;  // MEAN: 1 / (channels averaged)
 };
 
-__device__ __forceinline__ Work decode(int w, int tiles, int npass, int H, int D, int pw,
-                                       int dmax) {
+struct Work {
+  int n, y, g, x0, dp, Dp, js;
+};
+
+// work index w = (((n H + y) G + g) tiles + tile) npass + pass: consecutive items are
+// neighbouring segments of one row (and group), which share right-window columns in L2
+__device__ __forceinline__ Work decode(int w, const Args& a, int dmax) {
   Work k;
-  const int pass = w % npass;
-  const int rest = w / npass;
-  const int tile = rest % tiles;
-  const int row = rest / tiles;
-  k.y = row % H;
-  k.n = row / H;
+  const int pass = w % a.npass;
+  const int r1 = w / a.npass;
+  const int tile = r1 % a.tiles;
+  const int r2 = r1 / a.tiles;
+  k.g = r2 % a.G;
+  const int row = r2 / a.G;
+  k.y = row % a.H;
+  k.n = row / a.H;
   k.x0 = tile * kXT;
-  k.dp = pass * pw;
-  k.Dp = min(pw, D - k.dp);
+  k.dp = pass * a.pw;
+  k.Dp = min(a.pw, a.D - k.dp);
   k.js = k.x0 - k.dp - dmax;
   return k;
 }
@@ -117,54 +152,44 @@ __device__ __forceinline__ __attribute__((address_space(3))) unsigned* lds_word(
 }
 
 // a 4-pixel group of one channel row in registers: 16 B (fp32) or 8 B (fp16 / bf16)
-typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 template <typename T> struct Quad { using type = u32x2; };
 template <> struct Quad<float> { using type = f32x4v; };
 
 // Feature loads are issued by inline asm so that the compiler neither waits for them itself
 // (its control-flow merges would put vmcnt(0) -- a wait for every output store in flight --
 // in front of every step) nor knows them: the kernel counts vmcnt by hand (vm_wait).
-template <typename QT>
+template <bool ASM, typename QT>
 __device__ __forceinline__ void gload(QT& v, const void* p) {
-  if constexpr (sizeof(QT) == 16) {
+  if constexpr (!ASM) {  // compiler-tracked (the fused kernels: see band_h2)
+    typedef __attribute__((address_space(1))) const void gcvoid;
+    v = *reinterpret_cast<__attribute__((address_space(1))) const QT*>((gcvoid*)p);
+  } else if constexpr (sizeof(QT) == 16) {
     asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
   } else {
     asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
   }
 }
-// Wait for the feature loads: vmcnt(N) when N output stores were issued after them (they may
-// stay in flight), else vmcnt(0).  One asm statement with the scalar branch inside, and the
-// loaded registers as tied operands: no use of them is scheduled before the wait, and the
-// register allocator has a single place (the load's destination) to keep them.
-template <int N, typename QT>
-__device__ __forceinline__ void vm_wait(QT (&v)[8], int after_stores) {
+
+// Wait for the feature loads: vmcnt(N + NPF) when N output stores were issued after them (they
+// may stay in flight, as may the NPF touches issued right after the loads), else vmcnt(NPF).
+// One asm statement with the scalar branch inside, and the loaded registers (and the touch
+// destination) as tied operands: no use of them is scheduled before the wait, and the register
+// allocator has a single place (the load's destination) to keep them.
+template <int N, int NPF, bool ASM = true, typename QT>
+__device__ __forceinline__ void vm_wait(QT (&v)[8], unsigned& pf, int after_stores) {
+  if constexpr (!ASM) return;  // compiler-tracked loads: the compiler places the waits
   asm volatile(
-      "s_cmp_eq_u32 %8, 0\n\t"
+      "s_cmp_eq_u32 %9, 0\n\t"
       "s_cbranch_scc1 .Lvm_all%=\n\t"
-      "s_waitcnt vmcnt(%9)\n\t"
+      "s_waitcnt vmcnt(%10)\n\t"
       "s_branch .Lvm_done%=\n"
       ".Lvm_all%=:\n\t"
-      "s_waitcnt vmcnt(0)\n"
+      "s_waitcnt vmcnt(%11)\n"
       ".Lvm_done%=:"
       : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
-        "+v"(v[7])
-      : "s"(after_stores), "n"(N)
+        "+v"(v[7]), "+v"(pf)
+      : "s"(after_stores), "n"(N + NPF), "n"(NPF)
       : "memory", "scc");
-}
-
-template <typename T>
-__device__ __forceinline__ float4 quad_to_f32(typename Quad<T>::type q) {
-  if constexpr (sizeof(T) == 4) {
-    return make_float4(q.x, q.y, q.z, q.w);
-  } else if constexpr (std::is_same<T, __half>::value) {
-    // (a bit_cast of q.y to a 2 x __fp16 vector miscompiles to q.x with ROCm 7.2 clang)
-    const unsigned x = q.x, y = q.y;
-    auto f = [](unsigned short b) { return (float)__builtin_bit_cast(_Float16, b); };
-    return make_float4(f(x & 0xffffu), f(x >> 16), f(y & 0xffffu), f(y >> 16));
-  } else {  // bf16: the value is the high half of an fp32
-    return make_float4(__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u),
-                       __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u));
-  }
 }
 
 // 4 fp32 results -> storage type (round to nearest even; NaN stays NaN, overflow gives inf).
@@ -185,11 +210,20 @@ __device__ __forceinline__ void store_quad(T* p, f32x4v v) {
     *reinterpret_cast<__attribute__((address_space(1))) b4*>(g) = r;
   }
 }
+template <typename T>
+__device__ __forceinline__ void store_one(T* p, float v) {
+  typedef __attribute__((address_space(1))) void gvoid;
+  if constexpr (sizeof(T) == 4) {
+    *reinterpret_cast<__attribute__((address_space(1))) float*>((gvoid*)p) = v;
+  } else {
+    const T h = (T)v;
+    *reinterpret_cast<__attribute__((address_space(1))) unsigned short*>((gvoid*)p) =
+        __builtin_bit_cast(unsigned short, h);
+  }
+}
 
 template <typename T>
 __device__ __forceinline__ float ld1(const T* p) { return (float)*p; }
-template <typename T>
-__device__ __forceinline__ void st1(T* p, float v) { *p = (T)v; }
 
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
@@ -200,31 +234,44 @@ __device__ __forceinline__ float wave_max(float v) {
 // exponent e with x = f 2^e, f in [0.5, 1) (x > 0 finite)
 __device__ __forceinline__ int exp_of(float x) { return __builtin_amdgcn_frexp_expf(x); }
 
-template <typename T, int TMAX, bool MEAN>
-__global__ __launch_bounds__(kThreads, 2) void ip_band_h2(
-    const T* __restrict__ L, const T* __restrict__ R, T* __restrict__ out, int C,
-    int H, int W, int D, Strides4 ls, Strides4 rs, int tiles, int npass, int pw, int nwork,
-    int stagger) {
-  using G = Geo<TMAX>;
+// Workgroups per CU: two (each wave owns 256 registers), except the fused kernels, whose
+// online softmax does not fit beside the accumulators in 256: one, with 512 (VGPRs + AGPRs).
+template <bool FUSE>
+constexpr int wg_per_cu() {
+  return FUSE ? 1 : 2;
+}
+
+template <typename T, typename TO, int TMAX, bool MEAN, int LAYOUT, bool FUSE>
+__global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args) {
+  using G = Geo<T, TMAX>;
   constexpr int DMAX = G::DMAX;
+  constexpr int NP = G::NP;
+  // The fused kernels run one workgroup per CU with the accumulators partly in AGPRs, where the
+  // register allocator splits live ranges with copies: hand-counted asm loads (and L2 touches)
+  // are not safe there, so they use compiler-tracked loads.
+  constexpr bool ASM = !FUSE;
+  constexpr int PF = ASM ? kPF : 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const T* __restrict__ L = static_cast<const T*>(args.L);
+  const T* __restrict__ R = static_cast<const T*>(args.R);
+  TO* __restrict__ out = static_cast<TO*>(args.out);
+  const int cpg = args.cpg, H = args.H, W = args.W, D = args.D;
+  const Strides4 ls = args.ls, rs = args.rs;
 
   // work range of this workgroup's XCD group (blocks b and b+8 share an XCD): consecutive
   // segments of a row run on one XCD at the same time and share its L2 for the right window
   const int grp = blockIdx.x & 7;
   const int gi = blockIdx.x >> 3;
   const int gsz = gridDim.x >> 3;
-  const int q = nwork >> 3, rr = nwork & 7;
+  const int q = args.nwork >> 3, rr = args.nwork & 7;
   const int wbeg = grp < rr ? grp * (q + 1) : rr * (q + 1) + (grp - rr) * q;
   const int wend = wbeg + q + (grp < rr ? 1 : 0);
   if (wbeg + gi >= wend) return;  // the whole workgroup leaves together
   const int nitems = (wend - (wbeg + gi) + gsz - 1) / gsz;
-  const int nks = (C + kKC - 1) / kKC;
-  const int S = nitems * nks;  // pipeline steps of this workgroup
-  // the second workgroup of a CU starts later, so the two are not in phase (one streams its
-  // output while the other loads and multiplies)
-  if (stagger > 0 && blockIdx.x >= gridDim.x / 2)
-    for (int i = 0; i < stagger; ++i) __builtin_amdgcn_s_sleep(64);
+  const int nks = (cpg + kKC - 1) / kKC;
+  const bool store_vol = __builtin_amdgcn_readfirstlane(args.out != nullptr ? 1 : 0) != 0;
+  // NGHWD quads are 16-B aligned only when D % 4 == 0
+  const bool dq = LAYOUT == kNDHW || __builtin_amdgcn_readfirstlane(D & 3) == 0;
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -237,7 +284,7 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_h2(
   const int g = min(tid - ch * G::GROUPS, G::GROUPS - 1);  // rows 4g .. 4g+3
   const bool isR = 4 * g < G::RW;
   const int64_t cs = isR ? rs.c : ls.c;
-  const bool cfull = __builtin_amdgcn_readfirstlane(C % kKC) == 0;  // uniform: a scalar branch
+  const bool cfull = __builtin_amdgcn_readfirstlane(cpg % kKC) == 0;  // uniform: a scalar branch
 
   using QT = typename Quad<T>::type;
   struct Set {
@@ -245,99 +292,146 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_h2(
     int nv;  // valid channels of v (0: pixels outside the image or an idle lane)
   };
   Set st;  // one set: the loads of step s+1 fly during step s's matrix work
-  auto load = [&](Set& st, int s) {
-    s = min(s, S - 1);  // past the end: reload the last step (nobody consumes it)
-    const int it = s / nks;
-    const int c0 = (s - it * nks) * kKC + 8 * ch;
-    const Work k = decode(wbeg + gi + it * gsz, tiles, npass, H, D, pw, DMAX);
+  auto row_of = [&](const Work& k) {
+    return isR ? R + (int64_t)k.n * rs.n + (int64_t)k.y * rs.h
+               : L + (int64_t)k.n * ls.n + (int64_t)k.y * ls.h;
+  };
+  auto load = [&](Set& st, const Work& k, int ks) {
+    const int cl = ks * kKC + 8 * ch;  // channel within the group
     const int px = isR ? k.js + 4 * g : k.x0 + 4 * g - G::RW;
     const bool okp = active && px >= 0 && px < W;
-    const T* row = isR ? R + (int64_t)k.n * rs.n + (int64_t)k.y * rs.h
-                       : L + (int64_t)k.n * ls.n + (int64_t)k.y * ls.h;
-    const T* p = row + (okp ? px : 0) + (int64_t)min(c0, C - 1) * cs;
+    const T* p = row_of(k) + (okp ? px : 0) + ((int64_t)k.g * cpg + min(cl, cpg - 1)) * cs;
     if (SMCV_ABLATE & 2) p = L + 4 * (lane & 7);
-    st.nv = okp ? min(max(C - c0, 0), 8) : 0;
-    // channel tail: clamp to the last channel (one code path; put() zeroes the tail)
-    const int lim = cfull ? 7 : min(max(C - 1 - c0, 0), 7);
+    st.nv = okp ? min(max(cpg - cl, 0), 8) : 0;
+    // channel tail: clamp to the group's last channel (one code path; put() zeroes the tail)
+    const int lim = cfull ? 7 : min(max(cpg - 1 - cl, 0), 7);
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) gload(st.v[kk], p + min(kk, lim) * cs);
+    for (int kk = 0; kk < 8; ++kk) gload<ASM>(st.v[kk], p + min(kk, lim) * cs);
+  };
+  // Touch every 128-B line a later step loads: lane (ch, g) loads one dword of channel
+  // 8 ch + (g & 7) of its own pixel group -- the 8 groups of a line cover the line's 8
+  // channels -- so that step's real loads find their lines in L2.  Lanes with nothing to touch
+  // (and invalid steps) reload L[0]: every lane issues exactly kPF touches per step.
+  unsigned pfd = 0;  // the touches' destination: never read, live until the final wait
+  auto touch = [&](const Work& k, int ks, bool valid) {
+    if constexpr (PF != 0) {
+      const int cl = ks * kKC + 8 * ch + (g & 7);
+      const int px = isR ? k.js + 4 * g : k.x0 + 4 * g - G::RW;
+      const bool ok = valid && active && px >= 0 && px < W && cl < cpg;
+      const T* p = ok ? row_of(k) + px + ((int64_t)k.g * cpg + cl) * cs : L;
+      asm volatile("global_load_dword %0, %1, off" : "+v"(pfd) : "v"(p) : "memory");
+    }
   };
 
-  int kL = 0, kR = 0;  // per-segment scale exponents (workgroup-uniform)
-  float mx = 0.f;      // this lane's max|x| over the current segment
-  // split one step into the h / m planes (scaled by 2^k when k != 0)
+  int kL = 0, kR = 0;  // per-segment scale exponents (workgroup-uniform; fp32 only)
+  float mx = 0.f;      // this lane's max|x| over the current segment (fp32 only)
+  // stage one step into the plane(s)
   auto put = [&](Set& st) {
     if (!active) return;
-    float4 v[8];
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) v[kk] = quad_to_f32<T>(st.v[kk]);
-    if (__any(st.nv != 8)) {  // row edges / channel tail only
+    if constexpr (NP == 2) {
+      float4 v[8];
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk)
-        if (kk >= st.nv) v[kk] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+        v[kk] = make_float4(st.v[kk].x, st.v[kk].y, st.v[kk].z, st.v[kk].w);
+      if (__any(st.nv != 8)) {  // row edges / channel tail only
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk)
-      mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v[kk].x), fabsf(v[kk].y)),
-                           fmaxf(fabsf(v[kk].z), fabsf(v[kk].w))));
-    float col[4][8];
+        for (int kk = 0; kk < 8; ++kk)
+          if (kk >= st.nv) v[kk] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-      col[0][kk] = v[kk].x;
-      col[1][kk] = v[kk].y;
-      col[2][kk] = v[kk].z;
-      col[3][kk] = v[kk].w;
-    }
-    unsigned char* base = smem;
-    auto split = [&](float sc, auto scaled) {
+      for (int kk = 0; kk < 8; ++kk)
+        mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v[kk].x), fabsf(v[kk].y)),
+                             fmaxf(fabsf(v[kk].z), fabsf(v[kk].w))));
+      float col[4][8];
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        col[0][kk] = v[kk].x;
+        col[1][kk] = v[kk].y;
+        col[2][kk] = v[kk].z;
+        col[3][kk] = v[kk].w;
+      }
+      auto split = [&](float sc, auto scaled) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          uint4 wh, wm;
+          unsigned* ph = reinterpret_cast<unsigned*>(&wh);
+          unsigned* pm = reinterpret_cast<unsigned*>(&wm);
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            const float a = col[p][2 * qq], b = col[p][2 * qq + 1];
+            const float as = decltype(scaled)::value ? a * sc : a;
+            const float bs = decltype(scaled)::value ? b * sc : b;
+            const hp2 hv = __builtin_amdgcn_cvt_pkrtz(as, bs);
+            const float ra = __builtin_fmaf(a, sc, -(float)hv[0]);
+            const float rb = __builtin_fmaf(b, sc, -(float)hv[1]);
+            const hp2 mv = __builtin_amdgcn_cvt_pkrtz(ra, rb);
+            ph[qq] = __builtin_bit_cast(unsigned, hv);
+            pm[qq] = __builtin_bit_cast(unsigned, mv);
+          }
+          const int off = swz(4 * g + p, ch);
+          *reinterpret_cast<uint4*>(smem + off) = wh;
+          *reinterpret_cast<uint4*>(smem + G::PLANE + off) = wm;
+        }
+      };
+      if (__builtin_amdgcn_readfirstlane(kL | kR) == 0) {  // uniform: a scalar branch
+        split(1.0f, std::false_type{});
+      } else {
+        split(__builtin_ldexpf(1.0f, isR ? kR : kL), std::true_type{});
+      }
+    } else {
+      // 16-bit features as they are: 8 channels x 4 pixels -> 4 rows of 8 channels
+      u32x2 qv[8];
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) qv[kk] = st.v[kk];
+      if (__any(st.nv != 8)) {
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk)
+          if (kk >= st.nv) qv[kk] = u32x2{0u, 0u};
+      }
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
-        uint4 wh, wm;
-        unsigned* ph = reinterpret_cast<unsigned*>(&wh);
-        unsigned* pm = reinterpret_cast<unsigned*>(&wm);
+        uint4 w;
+        unsigned* pw = reinterpret_cast<unsigned*>(&w);
 #pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-          const float a = col[p][2 * qq], b = col[p][2 * qq + 1];
-          const float as = decltype(scaled)::value ? a * sc : a;
-          const float bs = decltype(scaled)::value ? b * sc : b;
-          const hp2 hv = __builtin_amdgcn_cvt_pkrtz(as, bs);
-          const float ra = __builtin_fmaf(a, sc, -(float)hv[0]);
-          const float rb = __builtin_fmaf(b, sc, -(float)hv[1]);
-          const hp2 mv = __builtin_amdgcn_cvt_pkrtz(ra, rb);
-          ph[qq] = __builtin_bit_cast(unsigned, hv);
-          pm[qq] = __builtin_bit_cast(unsigned, mv);
+        for (int j = 0; j < 4; ++j) {  // channels 2j (low half), 2j+1 (high half) of pixel p
+          const unsigned lo = p < 2 ? qv[2 * j].x : qv[2 * j].y;
+          const unsigned hi = p < 2 ? qv[2 * j + 1].x : qv[2 * j + 1].y;
+          pw[j] = __builtin_amdgcn_perm(hi, lo, (p & 1) ? 0x07060302u : 0x05040100u);
         }
-        const int off = swz(4 * g + p, ch);
-        *reinterpret_cast<uint4*>(base + off) = wh;
-        *reinterpret_cast<uint4*>(base + G::PLANE + off) = wm;
+        *reinterpret_cast<uint4*>(smem + swz(4 * g + p, ch)) = w;
       }
-    };
-    if (__builtin_amdgcn_readfirstlane(kL | kR) == 0) {  // uniform: a scalar branch
-      split(1.0f, std::false_type{});
-    } else {
-      split(__builtin_ldexpf(1.0f, isR ? kR : kL), std::true_type{});
     }
   };
 
   // ------------------------------------------------------------------- MFMA role of a wave
   const int lr = lane & 31;
   const int hh = lane >> 5;
-  const unsigned char* abase = smem + 32 * wave * kRowB + swz(lr, hh);            // + 1024 t
+  const unsigned char* abase = smem + 32 * wave * kRowB + swz(lr, hh);  // + 1024 t
   const unsigned char* bbase = smem + (G::RW + 32 * wave) * kRowB + swz(lr, hh);
+  using FV = typename std::conditional<std::is_same<T, __bf16>::value, bf16x8, f16x8>::type;
+  constexpr int NB = NP == 2 ? 2 : 4;  // fragment buffers: blocks read ahead of the MFMAs
   f32x16 acc[TMAX];
+  auto mma = [](FV a, FV b, f32x16 c) {
+    if constexpr (std::is_same<T, __bf16>::value) {
+      return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+    } else {
+      return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+    }
+  };
   auto band = [&](auto first) {
-    f16x8 bh = *reinterpret_cast<const f16x8*>(bbase);
-    f16x8 bm = *reinterpret_cast<const f16x8*>(bbase + G::PLANE);
-    f16x8 ah[3], am[3];
+    const FV bh = *reinterpret_cast<const FV*>(bbase);
+    FV bm = bh;
+    if constexpr (NP == 2) bm = *reinterpret_cast<const FV*>(bbase + G::PLANE);
+    FV ah[NB], am[NB];
     auto rd = [&](int t) {
-      ah[t % 3] = *reinterpret_cast<const f16x8*>(abase + 1024 * t);
-      am[t % 3] = *reinterpret_cast<const f16x8*>(abase + G::PLANE + 1024 * t);
+      ah[t % NB] = *reinterpret_cast<const FV*>(abase + 1024 * t);
+      if constexpr (NP == 2) am[t % NB] = *reinterpret_cast<const FV*>(abase + G::PLANE + 1024 * t);
     };
-    rd(0);
-    if (TMAX > 1) rd(1);
+#pragma unroll
+    for (int t = 0; t < NB - 1 && t < TMAX; ++t) rd(t);
 #pragma unroll
     for (int t = 0; t < TMAX; ++t) {
-      if (t + 2 < TMAX) rd(t + 2);
+      if (t + NB - 1 < TMAX) rd(t + NB - 1);
       __builtin_amdgcn_sched_barrier(0);
       if (!(SMCV_ABLATE & 1)) {
         f32x16 c;
@@ -346,9 +440,11 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_h2(
         } else {
           c = acc[t];
         }
-        c = __builtin_amdgcn_mfma_f32_32x32x16_f16(am[t % 3], bh, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[t % 3], bm, c, 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[t % 3], bh, c, 0, 0, 0);
+        if constexpr (NP == 2) {
+          c = mma(am[t % NB], bh, c);
+          c = mma(ah[t % NB], bm, c);
+        }
+        acc[t] = mma(ah[t % NB], bh, c);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -357,135 +453,315 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_h2(
   // ------------------------------------------------------------------------------ epilogue
   // Lane (lr, hh) holds, in block t, element i at R row jj = c_i + 4 hh (c_i = (i & 3) +
   // 8 (i >> 2)) and L column lr: local disparity dl = 32 (a + 1) + u - c_i with a = T-2-t and
-  // u = lr - 4 hh.  dl lies in chunk a+1 (row u - c_i) when u >= c_i, else in chunk a (row
-  // 32 + u - c_i).  Chunk m lives in ring slot (m + 3) % 3; for slot(a) != 2 the two slots are
-  // adjacent and the address is one base plus a compile-time offset.  Block a completes chunk
-  // a (chunk -1 and chunk T-1 hold only rows no one stores).
-  const unsigned ring0 = lds_addr(smem + G::RING);
+  // u = lr - 4 hh, i.e. chunk a+1 (row u - c_i) when u >= c_i, else chunk a (row 32 + u - c_i).
+  // Block a completes chunk a of the wave (chunk -1 and chunk T-1 hold only rows no one reads).
+  //   NDHW ring: [slot][32 d][32 x], chunk m in slot m % 3 (adjacent slots: one base + a
+  //   compile-time offset; slot 2 -> 0 wraps with one select);
+  //   NGHWD ring: [32 x][96 d, circular], chunk m at d-positions 32 (m % 3) .. +32.
+  // Both write patterns are conflict-free (132 / 388 B lane strides in a 32-lane half), and so
+  // are the 16-B readouts (scripts/check_h2_bounds.py).
+  const unsigned ringw = lds_addr(smem + G::RING) + (unsigned)(wave * kRingW);
   const int u = lr - 4 * hh;
-  const unsigned wbase = ring0 + 4u * (32 * wave + lr) + (unsigned)u * 512u;  // u >= -4
-  const int srow = 8 * wave + hh;  // this lane's first store row in a chunk (+2 qq)
-  const unsigned rbase = ring0 + (unsigned)srow * 512u + 16u * lr;
+  const unsigned wbase = LAYOUT == kNDHW ? ringw + (unsigned)(4 * lr + 128 * u)
+                                         : ringw + (unsigned)(384 * lr + 4 * u);
+  const int rl = lane >> 3, cl = lane & 7;  // chunk readout: rows (NDHW) / pixels (NGHWD) 8qq + rl
   const size_t plane_stride = (size_t)H * W;
+  // lane parts of the chunk store addresses, in elements (32-bit: the host keeps 8 H W < 2^31);
+  // the rest of each address is uniform (scalar registers)
+  const int lane_st = LAYOUT == kNDHW ? rl * H * W + 4 * cl : rl * D + 4 * cl;
+  const unsigned rdbase = LAYOUT == kNDHW ? ringw + (unsigned)(rl * 128 + 16 * cl)
+                                          : ringw + (unsigned)(rl * 384 + 16 * cl);
+
+  // fused soft-argmin state: pixels 4 cl + e of the wave, rows 8 qq + rl of every chunk
+  float fm[4];
+  double fs[4], ft[4];
+  int fnan = 0;
+  auto fuse_chunk = [&](int a, const f32x4v (&v)[4], int Dp, int rlo) {
+    // branch-free: selects only, so the block's code stays one basic block
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float vv[4];
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq)  // beyond D: not in the softmax
+        vv[qq] = 32 * a + 8 * qq + rlo < Dp ? v[qq][e] : -INFINITY;
+      const bool nn = (vv[0] != vv[0]) | (vv[1] != vv[1]) | (vv[2] != vv[2]) | (vv[3] != vv[3]);
+      fnan |= nn ? (1 << e) : 0;
+      const float nm = fmaxf(fm[e], fmaxf(fmaxf(vv[0], vv[1]), fmaxf(vv[2], vv[3])));
+      const bool fin = nm != -INFINITY && nm != INFINITY;
+      // rescale the running sums to the new maximum (factor 1 when it did not grow)
+      const float f = fin && fm[e] != -INFINITY ? expf(fm[e] - nm) : 0.f;
+      float ps = 0.f, pt = 0.f;  // this chunk, disparities relative to its row 32 a + rl
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const float ex = fin ? expf(vv[qq] - nm) : 0.f;
+        ps += ex;
+        pt = fmaf((float)(8 * qq), ex, pt);
+      }
+      fs[e] = fs[e] * (double)f + (double)ps;
+      ft[e] = ft[e] * (double)f + (double)(32 * a + rlo) * (double)ps + (double)pt;
+      fm[e] = nm;
+      __builtin_amdgcn_sched_barrier(0);  // one pixel at a time: bounded temporaries
+    }
+  };
+  auto fuse_finish = [&](const Work& k) {
+    fnan |= __shfl_xor(fnan, 8);
+    fnan |= __shfl_xor(fnan, 16);
+    fnan |= __shfl_xor(fnan, 32);
+    float dv[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float M = fm[e];
+      M = fmaxf(M, __shfl_xor(M, 8));
+      M = fmaxf(M, __shfl_xor(M, 16));
+      M = fmaxf(M, __shfl_xor(M, 32));
+      const double f =
+          (fm[e] == -INFINITY || M == INFINITY) ? 0.0 : (double)expf(fm[e] - M);
+      double s = fs[e] * f, t = ft[e] * f;
+      s += __shfl_xor(s, 8);
+      t += __shfl_xor(t, 8);
+      s += __shfl_xor(s, 16);
+      t += __shfl_xor(t, 16);
+      s += __shfl_xor(s, 32);
+      t += __shfl_xor(t, 32);
+      // NaN anywhere in the column, or an all -inf / any +inf column: NaN, as torch
+      dv[e] = (((fnan >> e) & 1) || M == INFINITY || M == -INFINITY) ? NAN : (float)(t / s);
+    }
+    if (rl == 0) {
+      const int x = k.x0 + 32 * wave + 4 * cl;
+      float* o = args.disp + ((size_t)k.n * H + k.y) * W + x;
+      if (x + 4 <= W) {
+        const f32x4v r = {dv[0], dv[1], dv[2], dv[3]};
+        store_quad<float>(o, r);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (x + e < W) store_one<float>(o + e, dv[e]);
+      }
+    }
+  };
 
   // SCALE: multiply back by 2^-(kL+kR); XLT: the segment has cells x < d (R pad rows), forced
-  // to 0 (an R pad row can meet a NaN).  Compile-time, so the common case costs no VALU.
+  // to 0.  Compile-time, so the common case costs no VALU.
   auto epilogue_v = [&](const Work& k, bool fast, auto scale, auto xlt) {
-    const bool fullx = k.x0 + kXT <= W;
-    T* const olane = out + ((size_t)k.n * D + k.dp + srow) * plane_stride +
-                         (size_t)k.y * W + k.x0 + 4 * lr;
-    const bool okx = k.x0 + 4 * lr < W;
-    const float mul = MEAN ? 1.0f / (float)C : 1.0f;
+    const int x0w = k.x0 + 32 * wave;  // this wave's first pixel
+    const float mul = args.mul;
     const int kk = -(kL + kR);
     const int jlane = k.js + 32 * wave + 4 * hh;  // R row of element c_i of block 0, minus c_i
+    if constexpr (FUSE) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        fm[e] = -INFINITY;
+        fs[e] = 0.0;
+        ft[e] = 0.0;
+      }
+      fnan = 0;
+    }
 #pragma unroll
     for (int t = TMAX - 1; t >= 0; --t) {
       const int a = TMAX - 2 - t;
-      const int sa = (a + 3) % 3, sb = (a + 4) % 3;  // slots of chunks a, a+1
-      unsigned wb = wbase;
-      asm volatile("" : "+v"(wb));  // per block: not hoisted (and spilled)
+      // per block, opaque to the compiler: the per-element addresses and selects below are
+      // recomputed in each block (two VALU each) instead of being hoisted out of the block loop
+      // as 16+ loop-invariant registers (which spill at two workgroups per CU)
+      unsigned wb = wbase, rb = rdbase;
+      int uu = u, jl = jlane, ls_ = lane_st, rlo = rl, clo = cl;
+      asm volatile("" : "+v"(wb), "+v"(uu), "+v"(jl), "+v"(rb), "+v"(ls_), "+v"(rlo), "+v"(clo));
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int ci = (i & 3) + 8 * (i >> 2);
         float val = acc[t][i];
         if (MEAN) val *= mul;
         if constexpr (decltype(scale)::value) val = __builtin_ldexpf(val, kk);
-        if constexpr (decltype(xlt)::value) val = jlane + 32 * t + ci >= 0 ? val : 0.f;
+        if constexpr (decltype(xlt)::value) val = jl + 32 * t + ci >= 0 ? val : 0.f;
         unsigned addr;
-        if (sa != 2) {  // ring0 + col + slot(a+1) kSlot + (u - c_i) 512, both cases
-          addr = wb + (unsigned)(sb * kSlot - ci * 512);
-        } else {  // chunk a in slot 2, chunk a+1 in slot 0
-          addr = wb + (unsigned)(3 * kSlot - ci * 512) - (u >= ci ? 3u * kSlot : 0u);
+        if constexpr (LAYOUT == kNDHW) {
+          const int sA = (a + 3) % 3, sB = (a + 4) % 3;  // slots of chunks a, a+1
+          if (sA != 2) {
+            addr = wb + (unsigned)(sB * kSlot - ci * 128);
+          } else {  // chunk a in slot 2, chunk a+1 in slot 0
+            addr = wb + (unsigned)(3 * kSlot - ci * 128) - (uu >= ci ? 3u * kSlot : 0u);
+          }
+        } else {
+          const int bp = 32 * ((a + 4) % 3);  // ring d-position of local disparity 32 (a+1)
+          if (bp != 0) {
+            addr = wb + (unsigned)(4 * (bp - ci));
+          } else {  // u < c_i wraps to the top of the 96-entry circle
+            addr = wb + (unsigned)(4 * (96 - ci)) - (uu >= ci ? 384u : 0u);
+          }
         }
         lds_store1(addr, val);
       }
-      __syncthreads();
+      // the wave's own ring writes precede its reads (LDS executes a wave's operations in order)
+      asm volatile("" ::: "memory");
       if (a >= 0) {
-        // chunk a is complete: this wave's quarter (8 rows, two per store instruction)
-        const unsigned rb = rbase + (unsigned)sa * kSlot;
         f32x4v v[4];
 #pragma unroll
-        for (int qq = 0; qq < 4; ++qq) v[qq] = lds_load4(rb + 1024u * qq);
-        T* ol = olane + (size_t)(32 * a) * plane_stride;
-        asm volatile("" : "+v"(ol));
-        if (fast) {  // every store valid: exactly 4 (T-1) per lane, counted by vm_wait
+        for (int qq = 0; qq < 4; ++qq) {
+          const unsigned ra = LAYOUT == kNDHW ? rb + (unsigned)((a % 3) * kSlot + 8 * qq * 128)
+                                              : rb + (unsigned)(8 * qq * 384 + (a % 3) * 128);
+          v[qq] = lds_load4(ra);
+        }
+        if constexpr (FUSE) fuse_chunk(a, v, k.Dp, rlo);
+        if (store_vol) {
+          if constexpr (LAYOUT == kNDHW) {
+            TO* ol = out + (((size_t)k.n * D + k.dp + 32 * a) * plane_stride +
+                            (size_t)k.y * W + x0w) + ls_;
+            // rows 8 apart: one uniform stride, the pointer stepped store by store (kept
+            // opaque, so no 64-bit per-row offsets are hoisted into registers)
+            const size_t st8 = (size_t)8 * plane_stride;
+            if (fast) {  // every store valid: exactly 4 (T-1) per lane, counted by vm_wait
 #pragma unroll
-          for (int qq = 0; qq < 4; ++qq) store_quad<T>(ol + (size_t)(2 * qq) * plane_stride, v[qq]);
-        } else {
+              for (int qq = 0; qq < 4; ++qq) {
+                asm volatile("" : "+v"(ol));
+                store_quad<TO>(ol, v[qq]);
+                ol += st8;
+              }
+            } else {
 #pragma unroll
-          for (int qq = 0; qq < 4; ++qq) {
-            const int dl = 32 * a + 2 * qq + srow;
-            if (dl < k.Dp && (fullx || okx) && !(SMCV_ABLATE & 4))
-              store_quad<T>(ol + (size_t)(2 * qq) * plane_stride, v[qq]);
+              for (int qq = 0; qq < 4; ++qq) {
+                asm volatile("" : "+v"(ol));
+                const int dl = 32 * a + 8 * qq + rlo;
+                if (dl < k.Dp && x0w + 4 * clo < W && !(SMCV_ABLATE & 4)) store_quad<TO>(ol, v[qq]);
+                ol += st8;
+              }
+            }
+          } else {
+            const size_t pix = (((size_t)k.n * args.G + k.g) * H + k.y) * (size_t)W + x0w;
+            TO* ol = out + (pix * (size_t)D + k.dp + 32 * a) + ls_;
+            asm volatile("" : "+v"(ol));
+            if (fast) {
+#pragma unroll
+              for (int qq = 0; qq < 4; ++qq) store_quad<TO>(ol + (size_t)(8 * qq) * D, v[qq]);
+            } else {
+              const int d0 = 32 * a + 4 * clo;
+#pragma unroll
+              for (int qq = 0; qq < 4; ++qq) {
+                if (x0w + 8 * qq + rlo >= W || (SMCV_ABLATE & 4)) continue;
+                if (d0 + 4 <= k.Dp && dq) {
+                  store_quad<TO>(ol + (size_t)(8 * qq) * D, v[qq]);
+                } else {
+#pragma unroll
+                  for (int e = 0; e < 4; ++e)
+                    if (d0 + e < k.Dp) store_one<TO>(ol + (size_t)(8 * qq) * D + e, v[qq][e]);
+                }
+              }
+            }
           }
         }
       }
+      // one block at a time (the live accumulators shrink block by block)
+      __builtin_amdgcn_sched_barrier(0);
     }
+    if constexpr (FUSE) fuse_finish(k);
   };
 
   auto epilogue = [&](const Work& k, bool fast) {
     using TT = std::true_type;
     using FF = std::false_type;
-    const bool sc = __builtin_amdgcn_readfirstlane(kL + kR) != 0;
     const bool xl = __builtin_amdgcn_readfirstlane(k.js) < 0;
-    if (sc) {
-      if (xl) epilogue_v(k, fast, TT{}, TT{});
-      else epilogue_v(k, fast, TT{}, FF{});
-    } else {
-      if (xl) epilogue_v(k, fast, FF{}, TT{});
-      else epilogue_v(k, fast, FF{}, FF{});
+    if constexpr (NP == 2) {
+      if (__builtin_amdgcn_readfirstlane(kL + kR) != 0) {
+        if (xl)
+          epilogue_v(k, fast, TT{}, TT{});
+        else
+          epilogue_v(k, fast, TT{}, FF{});
+        return;
+      }
     }
+    if (xl)
+      epilogue_v(k, fast, FF{}, TT{});
+    else
+      epilogue_v(k, fast, FF{}, FF{});
   };
 
   // exact fp32 path for a segment holding +-inf (or a scale fp32 cannot reach)
   auto slow_segment = [&](const Work& k) {
-    const float mul = MEAN ? 1.0f / (float)C : 1.0f;
-    const T* lrow = L + (int64_t)k.n * ls.n + (int64_t)k.y * ls.h;
-    const T* rrow = R + (int64_t)k.n * rs.n + (int64_t)k.y * rs.h;
-    for (int idx = tid; idx < k.Dp * kXT; idx += kThreads) {
-      const int dl = idx / kXT, x = k.x0 + idx % kXT, d = k.dp + dl;
-      if (x >= W) continue;
+    const float mul = MEAN ? args.mul : 1.0f;
+    const T* lrow = L + (int64_t)k.n * ls.n + (int64_t)k.y * ls.h + (int64_t)k.g * cpg * ls.c;
+    const T* rrow = R + (int64_t)k.n * rs.n + (int64_t)k.y * rs.h + (int64_t)k.g * cpg * rs.c;
+    auto cell = [&](int x, int d) {
       float s = 0.f;
       if (x >= d) {
-        for (int c = 0; c < C; ++c) s = __builtin_fmaf(ld1(lrow + (int64_t)c * ls.c + x),
-                                                       ld1(rrow + (int64_t)c * rs.c + x - d), s);
+        for (int c = 0; c < cpg; ++c)
+          s = __builtin_fmaf(ld1(lrow + (int64_t)c * ls.c + x),
+                             ld1(rrow + (int64_t)c * rs.c + x - d), s);
         s *= mul;
       }
-      st1(out + (((size_t)k.n * D + d) * H + k.y) * W + x, s);
+      return s;
+    };
+    if (store_vol) {
+      for (int idx = tid; idx < k.Dp * kXT; idx += kThreads) {
+        const int dl = idx / kXT, x = k.x0 + idx % kXT, d = k.dp + dl;
+        if (x >= W) continue;
+        const float s = cell(x, d);
+        if constexpr (LAYOUT == kNDHW) {
+          store_one<TO>(out + (((size_t)k.n * D + d) * H + k.y) * W + x, s);
+        } else {
+          store_one<TO>(out + ((((size_t)k.n * args.G + k.g) * H + k.y) * W + x) * D + d, s);
+        }
+      }
+    }
+    if constexpr (FUSE) {
+      for (int xx = tid; xx < kXT; xx += kThreads) {
+        const int x = k.x0 + xx;
+        if (x >= W) continue;
+        float m = -INFINITY;
+        double s = 0.0, t = 0.0;
+        bool nan = false;
+        for (int d = 0; d < k.Dp; ++d) {
+          const float v = cell(x, d);
+          nan |= v != v;
+          if (v > m) {
+            const double f = m == -INFINITY ? 0.0 : (double)expf(m - v);
+            s *= f;
+            t *= f;
+            m = v;
+          }
+          if (m != INFINITY && m != -INFINITY) {
+            const double e = (double)expf(v - m);
+            s += e;
+            t += (double)d * e;
+          }
+        }
+        store_one<float>(args.disp + ((size_t)k.n * H + k.y) * W + x,
+                         (nan || m == INFINITY || m == -INFINITY) ? NAN : (float)(t / s));
+      }
     }
   };
 
   // ----------------------------------------------------------------------------- main loop
   // maxima words: [0] max|L| parity 0, [1] max|R| parity 0, [2], [3] parity 1
   const unsigned maxw = lds_addr(smem + G::MAXW);
-  if (tid < 4) *reinterpret_cast<__attribute__((address_space(3))) unsigned*>(maxw + 4 * tid) = 0u;
+  if (tid < 4) *lds_word(maxw + 4 * tid) = 0u;
   bool redone = false;  // the current segment is a recomputation
   bool pend = false;    // 4 (T-1) output stores were issued after the outstanding feature loads
-  // one pipeline step; returns true when the segment must be recomputed from its first step
-  auto body = [&](int s) -> bool {
-    const int it = s / nks;
-    const int ks = s - it * nks;
-    const Work k = decode(wbeg + gi + it * gsz, tiles, npass, H, D, pw, DMAX);
+  // One pipeline step: channel step ks of item it (work k); nx / ks1 name the next step, whose
+  // loads this step issues (none after the last), pk / pks / pv the step after that, whose lines
+  // it touches.  Returns true when the segment must be recomputed from its first step.
+  auto body = [&](const Work& k, int it, int ks, const Work& nx, int ks1, bool more,
+                  const Work& pk, int pks, bool pv) -> bool {
     if (ks == 0) mx = 0.f;
     __syncthreads();  // A: the previous step's fragment reads are done
     SM_STAMP(0);
-    vm_wait<4 * (TMAX - 1)>(st.v, __builtin_amdgcn_readfirstlane((int)pend));
+    vm_wait<4 * (TMAX - 1), PF, ASM>(st.v, pfd, __builtin_amdgcn_readfirstlane((int)pend));
     pend = false;
     put(st);
     const unsigned par = (unsigned)(it & 1) * 8u;
-    if (ks == nks - 1) {
-      const float ml = wave_max(isR ? 0.f : mx), mr = wave_max(isR ? mx : 0.f);
-      if (lane == 0) {
-        __hip_atomic_fetch_max(lds_word(maxw + par), __float_as_uint(ml), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_fetch_max(lds_word(maxw + par + 4), __float_as_uint(mr), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
+    if constexpr (NP == 2) {
+      if (ks == nks - 1) {
+        const float ml = wave_max(isR ? 0.f : mx), mr = wave_max(isR ? mx : 0.f);
+        if (lane == 0) {
+          __hip_atomic_fetch_max(lds_word(maxw + par), __float_as_uint(ml), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_fetch_max(lds_word(maxw + par + 4), __float_as_uint(mr), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if (tid < 2)  // the next segment's words: last read before barrier A of this step
+          *lds_word(maxw + (8u - par) + 4 * tid) = 0u;
       }
-      if (tid < 2)  // the next segment's words: last read before barrier A of this step
-        *reinterpret_cast<__attribute__((address_space(3))) unsigned*>(maxw + (8u - par) + 4 * tid) = 0u;
     }
     SM_STAMP(1);
-    load(st, s + 1);
+    if (more) load(st, nx, ks1);
+    touch(pk, pks, pv);  // unconditional: vm_wait counts exactly kPF touches after the loads
     SM_STAMP(2);
     __syncthreads();  // B: the planes of step s are complete
     SM_STAMP(0);
@@ -495,46 +771,92 @@ __global__ __launch_bounds__(kThreads, 2) void ip_band_h2(
       band(std::false_type{});
     SM_STAMP(3);
     if (ks != nks - 1) return false;
-    // ---- end of a segment: range check, then the epilogue
-    const float ml = __uint_as_float(*reinterpret_cast<__attribute__((address_space(3))) unsigned*>(maxw + par));
-    const float mr = __uint_as_float(*reinterpret_cast<__attribute__((address_space(3))) unsigned*>(maxw + par + 4));
-    const bool fin = ml <= 3.4e38f && mr <= 3.4e38f;  // no +-inf staged
-    const int el = ml > 0.f ? exp_of(ml) : 0, er = mr > 0.f ? exp_of(mr) : 0;
-    const bool okl = ml == 0.f || (el + kL <= 15 && el + kL >= -1);
-    const bool okr = mr == 0.f || (er + kR <= 15 && er + kR >= -1);
-    if (fin && okl && okr) {
-      const bool fast = k.x0 + kXT <= W && k.Dp == DMAX && !(SMCV_ABLATE & 12);
+    // ---- end of a segment: (fp32) range check, then the epilogue
+    const bool fast =
+        store_vol && dq && k.x0 + kXT <= W && k.Dp == DMAX && !(SMCV_ABLATE & 12);
+    if constexpr (NP == 1) {
       if (!(SMCV_ABLATE & 8)) epilogue(k, fast);
       pend = fast;  // exactly 4 (T-1) stores per lane were issued after the loads
       SM_STAMP(4);
-      redone = false;
       return false;
+    } else {
+      const float ml = __uint_as_float(*lds_word(maxw + par));
+      const float mr = __uint_as_float(*lds_word(maxw + par + 4));
+      const bool fin = ml <= 3.4e38f && mr <= 3.4e38f;  // no +-inf staged
+      const int el = ml > 0.f ? exp_of(ml) : 0, er = mr > 0.f ? exp_of(mr) : 0;
+      const bool okl = ml == 0.f || (el + kL <= 15 && el + kL >= -1);
+      const bool okr = mr == 0.f || (er + kR <= 15 && er + kR >= -1);
+      if (fin && okl && okr) {
+        if (!(SMCV_ABLATE & 8)) epilogue(k, fast);
+        pend = fast;  // exactly 4 (T-1) stores per lane were issued after the loads
+        SM_STAMP(4);
+        redone = false;
+        return false;
+      }
+      const int nkl = ml > 0.f ? 13 - el : kL, nkr = mr > 0.f ? 13 - er : kR;
+      if (!fin || redone || nkl < -100 || nkl > 100 || nkr < -100 || nkr > 100) {
+        slow_segment(k);
+        redone = false;
+        return false;
+      }
+      kL = nkl;
+      kR = nkr;
+      redone = true;
+      __syncthreads();  // every wave has read the maxima before they are cleared
+      if (tid < 2) *lds_word(maxw + par + 4 * tid) = 0u;
+      return true;
     }
-    const int nkl = ml > 0.f ? 13 - el : kL, nkr = mr > 0.f ? 13 - er : kR;
-    if (!fin || redone || nkl < -100 || nkl > 100 || nkr < -100 || nkr > 100) {
-      slow_segment(k);
-      redone = false;
-      return false;
+  };
+
+  // the step m steps after (item i, step s): its work item and step; false past the last item
+  auto ahead = [&](int i, int s, int m, Work& w, int& ws) -> bool {
+    s += m;
+    while (s >= nks) {
+      s -= nks;
+      ++i;
     }
-    kL = nkl;
-    kR = nkr;
-    redone = true;
-    __syncthreads();  // every wave has read the maxima before they are cleared
-    if (tid < 2)
-      *reinterpret_cast<__attribute__((address_space(3))) unsigned*>(maxw + par + 4 * tid) = 0u;
+    ws = s;
+    if (i >= nitems) return false;
+    w = decode(wbeg + gi + i * gsz, args, DMAX);
     return true;
   };
 
-  load(st, 0);
-  for (int s = 0; s < S; ++s) {
-    if (body(s)) {  // recompute the segment: restart its steps
-      vm_wait<0>(st.v, 0);  // the registers must not have a load in flight when reloaded
-      s = (s / nks) * nks;
-      load(st, s);
-      --s;
+  // items it = 0 .. nitems-1 (work index wbeg + gi + it gsz), channel steps ks = 0 .. nks-1;
+  // every load() is followed by exactly kPF touches (of the step after the loaded one)
+  Work cur = decode(wbeg + gi, args, DMAX);
+  {
+    Work pk = cur;
+    int pks = 0;
+    const bool pv = ahead(0, 0, 1, pk, pks);
+    load(st, cur, 0);
+    touch(pk, pks, pv);
+  }
+  for (int it = 0, ks = 0; it < nitems;) {
+    const bool last = ks == nks - 1;
+    const bool more = !last || it + 1 < nitems;
+    const Work nx = last && more ? decode(wbeg + gi + (it + 1) * gsz, args, DMAX) : cur;
+    Work pk = cur;
+    int pks = 0;
+    const bool pv = ahead(it, ks, 2, pk, pks);
+    if (body(cur, it, ks, nx, last ? 0 : ks + 1, more, pk, pks, pv)) {  // recompute the segment
+      vm_wait<0, 0, ASM>(st.v, pfd, 0);  // no load in flight when the registers are reloaded
+      ks = 0;
+      Work pk1 = cur;
+      int pks1 = 0;
+      const bool pv1 = ahead(it, 0, 1, pk1, pks1);
+      load(st, cur, 0);
+      touch(pk1, pks1, pv1);
+      continue;
+    }
+    if (last) {
+      cur = nx;
+      ++it;
+      ks = 0;
+    } else {
+      ++ks;
     }
   }
-  vm_wait<0>(st.v, 0);  // the last (clamped) prefetch lands before its registers die
+  vm_wait<0, 0, ASM>(st.v, pfd, 0);  // nothing in flight when the registers die
   SM_STAMP_FLUSH
 }
 
@@ -552,36 +874,31 @@ int device_cus() {
   return cached[dev];
 }
 
-// start offset of the second workgroup per CU, in units of 64 x 64 cycles (diagnostic override:
-// STEREOCV_H2_STAGGER)
-int stagger_units() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("STEREOCV_H2_STAGGER");
-    v = e ? atoi(e) : 0;
-  }
-  return v;
-}
-
-template <typename T, int TMAX>
-int launch(const T* l, const T* r, T* o, int64_t N, int64_t C, int64_t H, int64_t W,
-           int64_t D, int64_t npass, int64_t pw, Strides4 ls, Strides4 rs, bool mean,
-           hipStream_t st) {
-  using G = Geo<TMAX>;
-  const int tiles = (int)ceil_div(W, kXT);
-  const int64_t nwork = (int64_t)tiles * H * N * npass;
-  if (nwork > INT32_MAX / 64) return fail(SM_EINVAL, "inner product: too much work for one launch");
-  auto kern = mean ? ip_band_h2<T, TMAX, true> : ip_band_h2<T, TMAX, false>;
+template <typename T, typename TO, int TMAX, bool MEAN, int LAYOUT, bool FUSE>
+int launch(Args a, int64_t N, hipStream_t st) {
+  using G = Geo<T, TMAX>;
+  a.tiles = (int)ceil_div(a.W, kXT);
+  const int64_t nwork = (int64_t)a.tiles * a.H * N * a.G * a.npass;
+  if (nwork > INT32_MAX / 64) return fail(SM_EINVAL, "band kernel: too much work for one launch");
+  a.nwork = (int)nwork;
+  auto kern = band_h2<T, TO, TMAX, MEAN, LAYOUT, FUSE>;
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::SHM);
   if (e != hipSuccess)
     return fail(SM_ELAUNCH, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
-  int64_t nwg = std::min<int64_t>(nwork, 2 * (int64_t)device_cus());
+  int64_t nwg = std::min<int64_t>(nwork, wg_per_cu<FUSE>() * (int64_t)device_cus());
   nwg = std::max<int64_t>(8, (nwg + 7) / 8 * 8);
-  hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(kThreads), G::SHM, st, l, r, o, (int)C,
-                     (int)H, (int)W, (int)D, ls, rs, tiles, (int)npass, (int)pw, (int)nwork,
-                     stagger_units());
-  return check_launch("ip_band_h2");
+  hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(kThreads), G::SHM, st, a);
+  return check_launch("band_h2");
+}
+
+// the smallest band geometry that holds one D pass of pw disparities
+template <typename F>
+int by_tmax(int64_t pw, F f) {
+  if (pw <= 32) return f(std::integral_constant<int, 2>{});
+  if (pw <= 64) return f(std::integral_constant<int, 3>{});
+  if (pw <= 128) return f(std::integral_constant<int, 5>{});
+  return f(std::integral_constant<int, 7>{});
 }
 
 }  // namespace h2band
@@ -590,41 +907,135 @@ int check_dot_args(const void* left, const void* right, const void* out, int dty
                    int64_t C, int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
                    const int64_t* r_strides, Strides4* ls, Strides4* rs);
 
-// Two-plane fp16 band kernel for fp32 / fp16 / bf16 features; *handled = false when the shape
-// needs the generic path (4-pixel groups: W % 4 == 0, 4-element aligned rows and base
-// pointers, C > 0).
-int band_h2_entry(const void* left, const void* right, void* out, int dtype, int64_t N, int64_t C,
-                  int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
-                  const int64_t* r_strides, int mode, void* stream, bool* handled) {
-  *handled = false;
+namespace {
+// Shared validation; *vec = the shape takes the band kernels (4-pixel groups: W % 4 == 0,
+// 4-element aligned rows and feature pointers, a 16-B aligned output, channels > 0).
+int h2_prepare(const void* left, const void* right, const void* out, int dtype, int64_t N,
+               int64_t C, int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
+               const int64_t* r_strides, h2band::Args* a, bool* vec) {
   Strides4 ls, rs;
   int rc = check_dot_args(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, &ls, &rs);
   if (rc) return rc;
   const uintptr_t align = 4 * (uintptr_t)elem_size(dtype);
-  const bool vec = (W % 4 == 0) && W >= 4 && C > 0 && ls.n % 4 == 0 && ls.c % 4 == 0 &&
-                   ls.h % 4 == 0 && rs.n % 4 == 0 && rs.c % 4 == 0 && rs.h % 4 == 0 &&
-                   ((reinterpret_cast<uintptr_t>(left) | reinterpret_cast<uintptr_t>(right)) % align == 0);
+  *vec = (W % 4 == 0) && W >= 4 && C > 0 && ls.n % 4 == 0 && ls.c % 4 == 0 && ls.h % 4 == 0 &&
+         rs.n % 4 == 0 && rs.c % 4 == 0 && rs.h % 4 == 0 &&
+         ((reinterpret_cast<uintptr_t>(left) | reinterpret_cast<uintptr_t>(right)) % align == 0) &&
+         reinterpret_cast<uintptr_t>(out) % 16 == 0 && 8 * H * W < INT32_MAX &&
+         8 * W * std::max<int64_t>(D, 1) < INT32_MAX;
+  // D passes of at most 192 disparities, balanced (D = 256: two passes of 128); a pass width
+  // that is a multiple of 4 keeps every right-window pixel group aligned
+  const int64_t npass = ceil_div(std::max<int64_t>(D, 1), (int64_t)192);
+  const int64_t pw = (ceil_div(std::max<int64_t>(D, 1), npass) + 3) / 4 * 4;
+  a->L = left;
+  a->R = right;
+  a->out = const_cast<void*>(out);
+  a->disp = nullptr;
+  a->C = (int)C;
+  a->cpg = (int)C;
+  a->G = 1;
+  a->H = (int)H;
+  a->W = (int)W;
+  a->D = (int)D;
+  a->ls = ls;
+  a->rs = rs;
+  a->tiles = 0;
+  a->npass = (int)npass;
+  a->pw = (int)pw;
+  a->nwork = 0;
+  a->mul = 1.0f;
+  return SM_OK;
+}
+}  // namespace
+
+// Inner product (mode 0, sum) / correlation (mode 1, mean) -> (N, D, H, W) in the input dtype.
+// *handled = false when the shape needs the generic path.
+int band_h2_entry(const void* left, const void* right, void* out, int dtype, int64_t N, int64_t C,
+                  int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
+                  const int64_t* r_strides, int mode, void* stream, bool* handled) {
+  using namespace h2band;
+  *handled = false;
+  Args a;
+  bool vec = false;
+  int rc = h2_prepare(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, &a, &vec);
+  if (rc) return rc;
   if (!vec) return SM_OK;
   *handled = true;
   if (N == 0 || H == 0 || D == 0) return SM_OK;
   const bool mean = mode == 1;
+  a.mul = 1.0f / (float)C;
   hipStream_t st = as_stream(stream);
-  using namespace h2band;
-  // D passes of at most 192 disparities, balanced (D = 256: two passes of 128); a pass width
-  // that is a multiple of 4 keeps every right-window pixel group aligned
-  const int64_t npass = ceil_div(D, (int64_t)192);
-  const int64_t pw = (ceil_div(D, npass) + 3) / 4 * 4;
   SM_DISPATCH_DTYPE(dtype, T0, {
     using T = typename std::conditional<std::is_same<T0, bf16_t>::value, __bf16, T0>::type;
-    const T* l = static_cast<const T*>(left);
-    const T* r = static_cast<const T*>(right);
-    T* o = static_cast<T*>(out);
-    if (pw <= 32) return launch<T, 2>(l, r, o, N, C, H, W, D, npass, pw, ls, rs, mean, st);
-    if (pw <= 64) return launch<T, 3>(l, r, o, N, C, H, W, D, npass, pw, ls, rs, mean, st);
-    if (pw <= 128) return launch<T, 5>(l, r, o, N, C, H, W, D, npass, pw, ls, rs, mean, st);
-    return launch<T, 7>(l, r, o, N, C, H, W, D, npass, pw, ls, rs, mean, st);
+    return by_tmax(a.pw, [&](auto tm) {
+      constexpr int TM = decltype(tm)::value;
+      return mean ? launch<T, T, TM, true, h2band::kNDHW, false>(a, N, st)
+                  : launch<T, T, TM, false, h2band::kNDHW, false>(a, N, st);
+    });
   });
   return SM_OK;
+}
+
+// Groupwise (mean over C/G contiguous channels) -> (N, G, H, W, D) float32.
+int band_h2_groupwise_entry(const void* left, const void* right, float* out, int dtype, int64_t N,
+                            int64_t C, int64_t H, int64_t W, int64_t D, int64_t G,
+                            const int64_t* l_strides, const int64_t* r_strides, void* stream,
+                            bool* handled) {
+  using namespace h2band;
+  *handled = false;
+  if (G <= 0 || C % G != 0) return fail(SM_EINVAL, "groupwise: C % G != 0");
+  Args a;
+  bool vec = false;
+  int rc = h2_prepare(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, &a, &vec);
+  if (rc) return rc;
+  if (!vec) return SM_OK;
+  *handled = true;
+  if (N == 0 || H == 0 || D == 0) return SM_OK;
+  a.G = (int)G;
+  a.cpg = (int)(C / G);
+  a.mul = 1.0f / (float)a.cpg;
+  hipStream_t st = as_stream(stream);
+  SM_DISPATCH_DTYPE(dtype, T0, {
+    using T = typename std::conditional<std::is_same<T0, bf16_t>::value, __bf16, T0>::type;
+    return by_tmax(a.pw, [&](auto tm) {
+      constexpr int TM = decltype(tm)::value;
+      return launch<T, float, TM, true, h2band::kNGHWD, false>(a, N, st);
+    });
+  });
+  return SM_OK;
+}
+
+// Inner product / correlation fused with soft-argmin: disparity (N, H, W) fp32, and the volume
+// when out != nullptr.  fp32 features, one D pass (D <= 192); *handled = false otherwise.
+int band_h2_fused_entry(const void* left, const void* right, void* out, float* disp, int dtype,
+                        int64_t N, int64_t C, int64_t H, int64_t W, int64_t D,
+                        const int64_t* l_strides, const int64_t* r_strides, int mode,
+                        void* stream, bool* handled) {
+  using namespace h2band;
+  *handled = false;
+  if (disp == nullptr && N * H * W > 0) return fail(SM_EINVAL, "null disparity pointer");
+  Args a;
+  bool vec = false;
+  // (the volume check of check_dot_args needs a pointer when only the disparity is wanted)
+  int rc = h2_prepare(left, right, out ? out : disp, dtype, N, C, H, W, D, l_strides, r_strides,
+                      &a, &vec);
+  if (rc) return rc;
+  if (N * H * W == 0) {
+    *handled = true;
+    return SM_OK;
+  }
+  vec = vec && reinterpret_cast<uintptr_t>(disp) % 16 == 0;
+  if (!vec || dtype != SM_F32 || a.npass != 1 || D == 0) return SM_OK;
+  *handled = true;
+  a.out = out;
+  a.disp = disp;
+  a.mul = 1.0f / (float)C;
+  const bool mean = mode == 1;
+  hipStream_t st = as_stream(stream);
+  return by_tmax(a.pw, [&](auto tm) {
+    constexpr int TM = decltype(tm)::value;
+    return mean ? launch<float, float, TM, true, h2band::kNDHW, true>(a, N, st)
+                : launch<float, float, TM, false, h2band::kNDHW, true>(a, N, st);
+  });
 }
 
 }  // namespace smcv

@@ -13,6 +13,7 @@ Reference operators mirrored (babiking/realtime_stereo_matcher):
   interweave_volume      model/mobile_stereo_net_v4.py:443-461 (shifted interweave, materialised)
   difference_volume      model/mobile_stereo_net.py:8-27 (+ _v2.py:8-27, _v3.py:9-28)
   correlation_volume     model/mobile_disp_net_c.py:188-205
+  inner_product_soft_argmin  either volume fused with soft_argmin
   soft_argmin            model/mobile_disp_net_c.py:208-220, model/mobile_stereo_net.py:144-147
   regression_presoftmax  model/mobile_stereo_net_v4.py:10-14
   hard_argmin/argmax     build-defined
@@ -153,6 +154,43 @@ def correlation_volume(l_fmap, r_fmap, max_disp):
         return out
 
     return _run(fn, left, right)
+
+
+def inner_product_soft_argmin(left, right, max_disparity, mean=False, keep_volume=True):
+    """Cost volume + soft-argmin in one kernel pass.
+
+    The inner-product volume (cost_volume/inner_product.py:11-42; ``mean=True``: the
+    correlation volume of model/mobile_disp_net_c.py:188-205) and its disparity regression
+    sum_d d * softmax_d(volume) (model/mobile_disp_net_c.py:208-220, = the inline soft-argmin of
+    model/mobile_stereo_net.py:144-147).  Returns ``(volume, disparity)``: the (N,D,H,W) volume
+    (``None`` with ``keep_volume=False``: it is then never written) and the (N,1,H,W) disparity,
+    both in the feature dtype.  fp32 features with W % 4 == 0 and D <= 192 run one fused band
+    kernel; other shapes run the volume and the regression kernels back to back.
+    """
+    left, right, dev, code = _pair(left, right, "inner_product_soft_argmin")
+    D = _disp(max_disparity, "inner_product_soft_argmin")
+    n, c, h, w = left.shape
+    mode = 1 if mean else 0
+
+    def call(vol, disp):
+        return _lib.load().sm_cv_inner_product_softargmin(
+            _ptr(left), _ptr(right), None if vol is None else _ptr(vol), _ptr(disp), code,
+            n, c, h, w, D, _lib.strides_arg(left), _lib.strides_arg(right), mode, _stream(dev))
+
+    def fn(keep):
+        vol = torch.empty((n, D, h, w), dtype=left.dtype, device=dev) if keep else None
+        disp = torch.empty((n, 1, h, w), dtype=left.dtype, device=dev)
+        if disp.numel():
+            rc = call(vol, disp)
+            if rc == _lib.SM_EUNSUPPORTED and vol is None:
+                # not a fused shape: the two-kernel path needs the volume in HBM for a moment
+                rc = call(torch.empty((n, D, h, w), dtype=left.dtype, device=dev), disp)
+            _lib.check(rc, "sm_cv_inner_product_softargmin")
+        return vol, disp
+
+    if keep_volume:
+        return _run(lambda: fn(True), left, right)
+    return None, _run(lambda: fn(False)[1], left, right)
 
 
 def groupwise_volume(left, right, n_groups, max_disparity):

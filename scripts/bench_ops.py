@@ -16,6 +16,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from realtime_stereo_matcher_amd import functional as F  # noqa: E402
 
 PEAK = 8.0e12
+MFMA_PEAK = 2.5e15  # dense bf16 / fp16 (MI355X_MICROARCH.md)
 
 
 def timeit(fn, reps, warm=3):
@@ -49,12 +50,14 @@ def main():
     only = set(filter(None, a.only.split(",")))
     rows = []
 
-    def run(name, fn, nbytes, **extra):
+    def run(name, fn, nbytes, flops=None, **extra):
         if only and name not in only:
             return
         med, best = timeit(fn, a.reps)
         rec = {"op": name, "median_us": med * 1e6, "best_us": best * 1e6, "alg_bytes": nbytes,
                "GBps": nbytes / med / 1e9, "roofline_frac": nbytes / med / PEAK}
+        if flops:  # valid-cell FLOPs against the dense bf16/fp16 MFMA peak
+            rec.update(TFLOPs=flops / med / 1e12, mfma_peak_frac=flops / med / MFMA_PEAK)
         rec.update(extra)
         rows.append(rec)
         print(json.dumps(rec), flush=True)
@@ -71,15 +74,18 @@ def main():
     prob = torch.softmax(vol, 1)
     run("regression_presoftmax_cfg2", lambda: F.regression_presoftmax(prob), vol_b + 540 * 960 * 4)
     del vol, prob
-    if hasattr(F, "inner_product_soft_argmin"):
-        run("fused_ip_softargmin_cfg2", lambda: F.inner_product_soft_argmin(L, R, 192), n_in + 540 * 960 * 4)
+    run("fused_ip_softargmin_cfg2", lambda: F.inner_product_soft_argmin(L, R, 192),
+        n_in + vol_b + 540 * 960 * 4)
+    run("fused_ip_softargmin_novol_cfg2",
+        lambda: F.inner_product_soft_argmin(L, R, 192, keep_volume=False), n_in + 540 * 960 * 4)
     del L, R
     torch.cuda.empty_cache()
 
     # cfg3: groupwise bf16 1x256x540x960 G=8 D=192 -> fp32 (N,G,H,W,D)
     L, R = feats((1, 256, 540, 960), torch.bfloat16)
     run("groupwise_bf16_cfg3", lambda: F.groupwise_volume(L, R, 8, 192),
-        2 * L.numel() * 2 + 8 * 540 * 960 * 192 * 4)
+        2 * L.numel() * 2 + 8 * 540 * 960 * 192 * 4,
+        flops=2 * 256 * 540 * sum(960 - d for d in range(192)))
     del L, R
     torch.cuda.empty_cache()
 

@@ -5,7 +5,7 @@ The feature loads are inline-asm `global_load_dwordx{2,4}` the compiler does not
 kernel relies on two properties of the generated code, checked here for every instantiation:
   1. no instruction touches a load's destination registers between the load and the next
      `s_waitcnt vmcnt` (a register copy there would read data that has not landed);
-  2. no wave ends (s_endpgm) with such a load still in flight;
+  2. no wave ends (s_endpgm) with such a load still in flight (the L2 touches included);
   3. no `flat_*` memory instruction exists (flat ops count in vmcnt out of order, which would
      break the `vmcnt(4 (T-1))` wait that lets the output stores stay in flight).
 A may-pending dataflow over the kernel's basic blocks carries each load to every instruction it
@@ -33,16 +33,26 @@ def regs(tok):
 
 
 def kernels(asm_text):
-    """(name, [(line_no, instruction)]) per ip_band_h2 instantiation."""
-    out, cur = [], None
+    """(name, [(line_no, instruction)]) per band_h2 instantiation.  Instructions that come from
+    an inline-asm statement (between ;;#ASMSTART and ;;#ASMEND) are tagged with a leading '@':
+    only those loads are hand-counted (the compiler waits for its own)."""
+    out, cur, in_asm = [], None, False
     for ln, line in enumerate(asm_text.splitlines(), 1):
-        if re.match(r"^_ZN4smcv6h2band10ip_band_h2.*:", line):
+        if re.match(r"^_ZN4smcv6h2band7band_h2.*:", line):
             cur = (line.split(":")[0], [])
             out.append(cur)
             continue
         if cur is None:
             continue
+        if ";;#ASMSTART" in line:
+            in_asm = True
+            continue
+        if ";;#ASMEND" in line:
+            in_asm = False
+            continue
         ins = line.split(";")[0].strip()
+        if in_asm and ins and not ins.startswith(".") and not ins.endswith(":"):
+            ins = "@" + ins
         if ins.startswith(".Lfunc_end"):
             cur = None
             continue
@@ -64,13 +74,13 @@ def blocks_of(body):
             labels[ins[:-1]] = len(blocks) - 1
             continue
         blocks[-1].append((ln, ins))
-        op = ins.split()[0]
+        op = ins.lstrip("@").split()[0]
         if op.startswith(("s_branch", "s_cbranch", "s_endpgm", "s_setpc")):
             blocks.append([])
     succ = []
     for i, b in enumerate(blocks):
         s = set()
-        last = b[-1][1].split() if b else []
+        last = b[-1][1].lstrip("@").split() if b else []
         op = last[0] if last else ""
         if op.startswith(("s_branch", "s_cbranch")):
             s.add(labels[last[1]])
@@ -83,6 +93,8 @@ def blocks_of(body):
 def transfer(block, pending, report=None):
     pending = set(pending)
     for ln, ins in block:
+        hand = ins.startswith("@")  # from an inline-asm statement
+        ins = ins.lstrip("@")
         op = ins.split()[0]
         if report is not None and op.startswith("flat_"):
             report.append(f"{ln}: flat memory op: {ins}")
@@ -92,7 +104,7 @@ def transfer(block, pending, report=None):
         if op == "s_endpgm" and pending and report is not None:
             report.append(f"{ln}: wave ends with loads in flight into v{sorted(pending)[:4]}...")
         toks = [t.strip(",") for t in ins.split()[1:]]
-        if op in ("global_load_dwordx4", "global_load_dwordx2"):
+        if hand and op in ("global_load_dwordx4", "global_load_dwordx2", "global_load_dword"):
             srcs = set()
             for t in toks[1:]:
                 srcs |= regs(t)
@@ -148,6 +160,9 @@ def main():
         print(b)
     n = len(kernels(asm))
     print(f"{n} kernels checked, {len(bad)} problems")
+    if n == 0:
+        print("no band_h2 kernels found in the asm (renamed?)")
+        return 1
     return 1 if bad else 0
 
 

@@ -1,24 +1,31 @@
 #!/usr/bin/env python3
-"""Host-side replay of the fp16 two-plane band kernel's indexing (csrc/ip_h2.hip), run before any
-GPU launch of a changed indexing scheme:   python scripts/check_h2_bounds.py
+"""Host-side replay of the band kernels' indexing (csrc/ip_h2.hip), run before any GPU launch of
+a changed indexing scheme:   python scripts/check_h2_bounds.py
 
-1. every stage lane's feature loads for every pipeline step of every workgroup stay inside the
-   feature tensor (the grid is 2 workgroups per CU);
-2. the epilogue's ring writes and reads stay inside the ring, and after block a the ring chunk
-   a holds, at (row, column), exactly the accumulator element of band cell (dl = 32a + row, x):
-   R row j = x - d (the shear permutation), for every wave and lane;
-3. every stored output offset lies inside the (N, D, H, W) volume and every (d, x) cell with
-   d < D, x < W of every segment is stored exactly once over the whole grid."""
+1. every stage lane's feature loads and L2 touches, for every step of every workgroup, stay
+   inside the feature tensor and inside the lane's channel group -- for the (N, D, H, W) kernels
+   (G = 1) and the groupwise kernel (G groups of C/G channels); the grid is 2 workgroups per CU;
+2. each wave's epilogue ring: every write and read stays inside the wave's ring, and after
+   block a the ring holds chunk a exactly -- the accumulator element of band cell
+   (dl = 32 a + row, x) -- in both layouts (NDHW [slot][d][x], NGHWD [x][d circular]); the ring
+   writes are bank-conflict free per 32-lane half (ds_write_b32) and the readouts per
+   ds_read_b128 lane group (MI355X_MICROARCH.md, LDS table);
+3. every stored volume offset lies inside the volume and every cell (d < D, x < W) of every
+   (n, g, y) row is stored exactly once over the whole grid, in both layouts, and the fused
+   kernel stores every disparity exactly once."""
 import sys
 
 import numpy as np
 
-KXT, KSLOT = 128, 32 * 512
+KXT, KSLOT = 128, 4096
+_G1 = list(range(0, 4)) + list(range(12, 16)) + list(range(20, 28))
+_G2 = list(range(4, 12)) + list(range(16, 20)) + list(range(28, 32))
+B128_GROUPS = [_G1, _G2, [l + 32 for l in _G1], [l + 32 for l in _G2]]
 
 
 def geo(D):
-    npass = -(-D // 192)
-    pw = (-(-D // npass) + 3) // 4 * 4
+    npass = -(-max(D, 1) // 192)
+    pw = (-(-max(D, 1) // npass) + 3) // 4 * 4
     T = 2 if pw <= 32 else 3 if pw <= 64 else 5 if pw <= 128 else 7
     DMAX = 32 * (T - 1)
     RW = KXT + DMAX
@@ -26,10 +33,10 @@ def geo(D):
     return T, DMAX, RW, ROWS // 4, npass, pw
 
 
-def work_lists(N, H, W, D, ncu):
+def work_lists(N, G, H, W, D, ncu):
     T, DMAX, RW, GROUPS, npass, pw = geo(D)
     tiles = -(-W // KXT)
-    nwork = tiles * H * N * npass
+    nwork = tiles * H * N * G * npass
     nwg = max(8, (min(nwork, 2 * ncu) + 7) // 8 * 8)
     q, rr = nwork >> 3, nwork & 7
     for blk in range(nwg):
@@ -42,130 +49,185 @@ def work_lists(N, H, W, D, ncu):
         yield blk, [wbeg + gi + it * gsz for it in range(nitems)]
 
 
-def decode(w, tiles, npass, H, D, pw, DMAX):
-    pas, rest = w % npass, w // npass
-    tile, row = rest % tiles, rest // tiles
+def decode(w, tiles, npass, G, H, D, pw, DMAX):
+    pas, r1 = w % npass, w // npass
+    tile, r2 = r1 % tiles, r1 // tiles
+    g, row = r2 % G, r2 // G
     y, n = row % H, row // H
     x0, dp = tile * KXT, pas * pw
-    return n, y, x0, dp, min(pw, D - dp), x0 - dp - DMAX
+    return n, y, g, x0, dp, min(pw, D - dp), x0 - dp - DMAX
 
 
-def check_loads(N, C, H, W, D, ncu=256):
+def check_loads(N, C, H, W, D, G=1, ncu=256):
     T, DMAX, RW, GROUPS, npass, pw = geo(D)
     tiles = -(-W // KXT)
     ITEMS = 2 * GROUPS
+    cpg = C // G
     cs, hs, ns = H * W, W, C * H * W
     numel = N * ns
-    nks = -(-C // 16)
+    nks = -(-cpg // 16)
     bad = 0
-    for blk, items in work_lists(N, H, W, D, ncu):
-        S = len(items) * nks
-        for s in range(S + 2):
-            ss = min(s, S - 1)
-            it, ks = divmod(ss, nks)
-            n, y, x0, dp, Dp, js = decode(items[it], tiles, npass, H, D, pw, DMAX)
-            for sq in range(256):
-                h = min(sq // GROUPS, 1)
-                g = min(sq - h * GROUPS, GROUPS - 1)
-                active = sq < ITEMS
-                isR = 4 * g < RW
-                c0 = ks * 16 + 8 * h
-                px = js + 4 * g if isR else x0 + 4 * g - RW
-                okp = active and 0 <= px < W
-                if okp and px % 4:
-                    bad += 1  # 16-B groups must be aligned
-                base = n * ns + y * hs + (px if okp else 0) + min(c0, C - 1) * cs
-                for kk in range(8):
-                    off = kk if C % 16 == 0 else min(kk, max(C - 1 - c0, 0))
-                    e = base + off * cs
-                    if e < 0 or e + 4 > numel:
-                        bad += 1
+    for blk, items in work_lists(N, G, H, W, D, ncu):
+        for w in items:
+            n, y, g, x0, dp, Dp, js = decode(w, tiles, npass, G, H, D, pw, DMAX)
+            for ks in range(nks):
+                for sq in range(256):
+                    h = min(sq // GROUPS, 1)
+                    gr = min(sq - h * GROUPS, GROUPS - 1)
+                    active = sq < ITEMS
+                    isR = 4 * gr < RW
+                    cl = ks * 16 + 8 * h
+                    px = js + 4 * gr if isR else x0 + 4 * gr - RW
+                    okp = active and 0 <= px < W
+                    if okp and px % 4:
+                        bad += 1  # 4-pixel groups must be aligned
+                    rowb = n * ns + y * hs
+                    base = rowb + (px if okp else 0) + (g * cpg + min(cl, cpg - 1)) * cs
+                    lim = 7 if cpg % 16 == 0 else min(max(cpg - 1 - cl, 0), 7)
+                    for kk in range(8):
+                        chn = g * cpg + min(cl, cpg - 1) + min(kk, lim)
+                        e = base + min(kk, lim) * cs
+                        if e < 0 or e + 4 > numel or not g * cpg <= chn < (g + 1) * cpg:
+                            bad += 1
+                    # the L2 touch of this step: channel cl + (gr & 7) of the same pixel group
+                    ct = cl + (gr & 7)
+                    if active and 0 <= px < W and ct < cpg:
+                        e = rowb + px + (g * cpg + ct) * cs
+                        if e < 0 or e + 1 > numel:
+                            bad += 1
     return bad
 
 
-def check_shear(T):
-    """Simulate the ring of one full segment; returns the number of mismatches."""
+def ring_addr(layout, a, lr, hh, ci):
+    u = lr - 4 * hh
+    if layout == 0:
+        wbase = 4 * lr + 128 * u
+        sa, sb = (a + 3) % 3, (a + 4) % 3
+        if sa != 2:
+            return wbase + sb * KSLOT - ci * 128
+        return wbase + 3 * KSLOT - ci * 128 - (3 * KSLOT if u >= ci else 0)
+    wbase = 384 * lr + 4 * u
+    bp = 32 * ((a + 4) % 3)
+    if bp:
+        return wbase + 4 * (bp - ci)
+    return wbase + 4 * (96 - ci) - (384 if u >= ci else 0)
+
+
+def read_addr(layout, a, lane, qq):
+    """(byte address of the 16-B read, pixel of element 0, local disparity of element 0,
+    pixel step, disparity step) of lane's read qq of chunk a"""
+    rl, cl = lane >> 3, lane & 7
+    if layout == 0:
+        return (a % 3) * KSLOT + (8 * qq + rl) * 128 + 16 * cl, 4 * cl, 32 * a + 8 * qq + rl, 1, 0
+    return (8 * qq + rl) * 384 + (a % 3) * 128 + 16 * cl, 8 * qq + rl, 32 * a + 4 * cl, 0, 1
+
+
+def check_shear(T, layout):
+    """One wave's ring over a whole segment; returns (mismatches, conflicted lane groups)."""
     DMAX = 32 * (T - 1)
-    ring = {}  # byte offset within the ring -> (wave, t, i, lane)
-    bad = 0
+    ring = {}
+    bad = conflicts = 0
     for a in range(-1, T - 1):
         t = T - 2 - a
-        sa, sb = (a + 3) % 3, (a + 4) % 3
-        for wave in range(4):
-            for lane in range(64):
-                lr, hh = lane & 31, lane >> 5
-                u = lr - 4 * hh
-                wbase = 4 * (32 * wave + lr) + u * 512
-                for i in range(16):
-                    ci = (i & 3) + 8 * (i >> 2)
-                    if sa != 2:
-                        addr = wbase + sb * KSLOT - ci * 512
-                    else:
-                        addr = wbase + 3 * KSLOT - ci * 512 - (3 * KSLOT if u >= ci else 0)
-                    if not 0 <= addr < 3 * KSLOT:
+        for i in range(16):
+            ci = (i & 3) + 8 * (i >> 2)
+            for hh in range(2):
+                banks = set()
+                for lr in range(32):
+                    addr = ring_addr(layout, a, lr, hh, ci)
+                    if not 0 <= addr < 3 * KSLOT or addr % 4:
                         bad += 1
                         continue
-                    ring[addr] = (wave, t, ci + 4 * hh, lr)
+                    banks.add((addr // 4) % 32)
+                    ring[addr] = (t, ci + 4 * hh, lr)  # block, R row in the block, L column
+                conflicts += len(banks) != 32
         if a < 0:
             continue
-        # chunk a is read: rows 8w + hh + 2qq, column 4 lr .. 4 lr + 3
-        for wave in range(4):
+        for qq in range(4):
+            for grp in B128_GROUPS:
+                banks = set()
+                for lane in grp:
+                    addr0 = read_addr(layout, a, lane, qq)[0]
+                    banks |= {(addr0 // 4 + e) % 64 for e in range(4)}
+                conflicts += len(banks) != 64
             for lane in range(64):
-                lr, hh = lane & 31, lane >> 5
-                srow = 8 * wave + hh
-                for qq in range(4):
-                    row = srow + 2 * qq
-                    dl = 32 * a + row
-                    for e in range(4):
-                        addr = sa * KSLOT + row * 512 + 16 * lr + 4 * e
-                        xcol = 4 * lr + e  # column within the segment
-                        src = ring.get(addr)
-                        if src is None:
-                            bad += 1
-                            continue
-                        w2, t2, jj, x2 = src
-                        # the element holds R row 32(w2+t2)+jj (relative to js) and L column
-                        # 32 w2 + x2; its disparity relative to dp is x - j + DMAX - ... :
-                        # d_l = (32 w2 + x2) - (32 (w2 + t2) + jj) + DMAX
-                        d_l = (32 * w2 + x2) - (32 * (w2 + t2) + jj) + DMAX
-                        if 32 * w2 + x2 != xcol or d_l != dl:
-                            bad += 1
-    return bad
+                addr0, x, dl, dx, dd = read_addr(layout, a, lane, qq)
+                if addr0 % 16 or not 0 <= addr0 < 3 * KSLOT:
+                    bad += 1
+                    continue
+                for e in range(4):
+                    src = ring.get(addr0 + 4 * e)
+                    if src is None:
+                        bad += 1
+                        continue
+                    t2, jj, x2 = src
+                    # wave-relative: L column x2, R row 32 t2 + jj, the window starting DMAX
+                    # before the wave's first pixel: d_l = x2 - (32 t2 + jj) + DMAX
+                    if x2 != x + e * dx or x2 - 32 * t2 - jj + DMAX != dl + e * dd:
+                        bad += 1
+    return bad, conflicts
 
 
-def check_stores(N, H, W, D, ncu=256):
+def check_stores(N, H, W, D, G=1, layout=0, ncu=256):
     T, DMAX, RW, GROUPS, npass, pw = geo(D)
     tiles = -(-W // KXT)
-    hits = np.zeros(N * D * H * W, np.int32)
+    size = N * G * H * W * D
+    hits = np.zeros(size, np.int32)
+    disp = np.zeros(N * H * W, np.int32)
+    dq = layout == 0 or D % 4 == 0
     bad = 0
-    for blk, items in work_lists(N, H, W, D, ncu):
+
+    def hit(o, cnt):
+        nonlocal bad
+        if o < 0 or o + cnt > size:
+            bad += 1
+            return
+        hits[o:o + cnt] += 1
+
+    for blk, items in work_lists(N, G, H, W, D, ncu):
         for w in items:
-            n, y, x0, dp, Dp, js = decode(w, tiles, npass, H, D, pw, DMAX)
-            fullx = x0 + KXT <= W
-            for a in range(T - 1):
-                for wave in range(4):
+            n, y, g, x0, dp, Dp, js = decode(w, tiles, npass, G, H, D, pw, DMAX)
+            fast = dq and x0 + KXT <= W and Dp == DMAX
+            for wave in range(4):
+                x0w = x0 + 32 * wave
+                for a in range(T - 1):
                     for lane in range(64):
-                        lr, hh = lane & 31, lane >> 5
-                        srow = 8 * wave + hh
-                        okx = x0 + 4 * lr < W
+                        rl, cl = lane >> 3, lane & 7
                         for qq in range(4):
-                            dl = 32 * a + 2 * qq + srow
-                            if dl < Dp and (fullx or okx):
-                                base = ((n * D + dp + dl) * H + y) * W + x0 + 4 * lr
-                                if base < 0 or base + 4 > hits.size:
-                                    bad += 1
-                                    continue
-                                hits[base:base + 4] += 1
+                            if layout == 0:
+                                dl = 32 * a + 8 * qq + rl
+                                if fast or (dl < Dp and x0w + 4 * cl < W):
+                                    hit(((n * D + dp + dl) * H + y) * W + x0w + 4 * cl, 4)
+                            else:
+                                pix = x0w + 8 * qq + rl
+                                d0 = 32 * a + 4 * cl
+                                o = (((n * G + g) * H + y) * W + pix) * D + dp + d0
+                                if fast or (pix < W and d0 + 4 <= Dp and dq):
+                                    hit(o, 4)
+                                elif pix < W:
+                                    for e in range(4):
+                                        if d0 + e < Dp:
+                                            hit(o + e, 1)
+                if layout == 0 and npass == 1:  # the fused kernel's disparities: lanes rl == 0
+                    for cl in range(8):
+                        x = x0w + 4 * cl
+                        for e in range(4):
+                            if x + e < W:
+                                disp[(n * H + y) * W + x + e] += 1
     bad += int((hits != 1).sum())
+    if layout == 0 and npass == 1:
+        bad += int((disp != 1).sum())
     return bad
 
 
 if __name__ == "__main__":
     fails = 0
-    for T in (2, 3, 5, 7):
-        b = check_shear(T)
-        print(f"shear T={T}: mismatches {b}")
-        fails += b
+    for layout in (0, 1):
+        for T in (2, 3, 5, 7):
+            b, c = check_shear(T, layout)
+            print(f"shear {'NDHW ' if layout == 0 else 'NGHWD'} T={T}: mismatches {b}, "
+                  f"conflicted lane groups {c}")
+            fails += b + c
     shapes = [(1, 32, 64, 128, 24), (1, 64, 2, 200, 192), (1, 32, 2, 100, 300), (1, 8, 2, 64, 64),
               (2, 20, 3, 260, 100), (1, 48, 2, 132, 33), (1, 16, 1, 1000, 256), (1, 7, 2, 36, 40),
               (1, 64, 2, 960, 192), (1, 33, 2, 512, 31), (1, 64, 3, 960, 192), (2, 17, 3, 64, 24),
@@ -174,5 +236,12 @@ if __name__ == "__main__":
         b = check_loads(*sh)
         st = check_stores(sh[0], sh[2], sh[3], sh[4])
         print(sh, "out-of-bounds loads:", b, " store coverage errors:", st)
+        fails += b + st
+    gshapes = [(1, 32, 3, 260, 100, 4), (2, 48, 2, 132, 33, 3), (1, 256, 2, 960, 192, 8),
+               (1, 16, 2, 64, 256, 2), (1, 24, 2, 200, 40, 8), (1, 40, 2, 128, 7, 5)]
+    for N, C, H, W, D, G in gshapes:
+        b = check_loads(N, C, H, W, D, G)
+        st = check_stores(N, H, W, D, G, layout=1)
+        print((N, C, H, W, D, G), "groupwise out-of-bounds loads:", b, " store coverage errors:", st)
         fails += b + st
     sys.exit(1 if fails else 0)

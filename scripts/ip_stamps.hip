@@ -13,28 +13,56 @@ __device__ unsigned long long g_stamps[4096][kStampPhases];
 }
 
 #include <cstdio>
+#include <cstdint>
 #include <cstring>
 #include <vector>
 
 int main(int argc, char** argv) {
-  const int64_t N = 1, C = 64, H = 540, W = 960, D = argc > 1 ? atoi(argv[1]) : 192;
-  const size_t nin = N * C * H * W, nout = N * D * H * W;
-  float *L, *R, *O;
-  hipMalloc(&L, nin * 4);
-  hipMalloc(&R, nin * 4);
+  // modes: bf16x3 (default), f32, h2 (inner product), fused (+ soft-argmin, volume kept),
+  // fusednv (soft-argmin only), gw (groupwise bf16 cfg3: C=256, G=8, fp32 (N,G,H,W,D) out)
+  const char* mode = argc > 2 ? argv[2] : "bf16x3";
+  const bool gw = !strcmp(mode, "gw");
+  const int64_t N = 1, C = gw ? 256 : 64, H = 540, W = 960, D = argc > 1 ? atoi(argv[1]) : 192;
+  const int64_t G = 8;
+  const size_t nin = N * C * H * W, nout = gw ? N * G * H * W * D : N * D * H * W;
+  const size_t esz = gw ? 2 : 4;
+  void *L, *R;
+  float *O, *disp;
+  hipMalloc(&L, nin * esz);
+  hipMalloc(&R, nin * esz);
   hipMalloc(&O, nout * 4);
-  const bool f32 = argc > 2 && !strcmp(argv[2], "f32");
-  const bool h2 = argc > 2 && !strcmp(argv[2], "h2");
+  hipMalloc(&disp, N * H * W * 4);
+  const bool f32 = !strcmp(mode, "f32");
+  const bool h2 = !strcmp(mode, "h2");
+  const bool fused = !strcmp(mode, "fused"), fusednv = !strcmp(mode, "fusednv");
+  const bool band = h2 || fused || fusednv || gw;
   bool handled = false;
   auto run = [&]() {
     if (h2) return smcv::band_h2_entry(L, R, O, SM_F32, N, C, H, W, D, nullptr, nullptr, 0, nullptr, &handled);
+    if (fused || fusednv)
+      return smcv::band_h2_fused_entry(L, R, fused ? O : nullptr, disp, SM_F32, N, C, H, W, D, nullptr,
+                                       nullptr, 0, nullptr, &handled);
+    if (gw)
+      return smcv::band_h2_groupwise_entry(L, R, O, SM_BF16, N, C, H, W, D, G, nullptr, nullptr, nullptr,
+                                           &handled);
     if (f32) return smcv::band_f32_entry(L, R, O, SM_F32, N, C, H, W, D, nullptr, nullptr, 0, nullptr, &handled);
     return smcv::band_mfma_entry(L, R, O, SM_F32, N, C, H, W, D, nullptr, nullptr, 0, nullptr);
   };
   std::vector<float> h(nin);
   for (size_t i = 0; i < nin; ++i) h[i] = (float)((i * 2654435761u) % 2001) / 1000.f - 1.f;
-  hipMemcpy(L, h.data(), nin * 4, hipMemcpyHostToDevice);
-  hipMemcpy(R, h.data(), nin * 4, hipMemcpyHostToDevice);
+  if (gw) {
+    std::vector<uint16_t> hb(nin);
+    for (size_t i = 0; i < nin; ++i) {
+      uint32_t u;
+      memcpy(&u, &h[i], 4);
+      hb[i] = (uint16_t)(u >> 16);
+    }
+    hipMemcpy(L, hb.data(), nin * 2, hipMemcpyHostToDevice);
+    hipMemcpy(R, hb.data(), nin * 2, hipMemcpyHostToDevice);
+  } else {
+    hipMemcpy(L, h.data(), nin * 4, hipMemcpyHostToDevice);
+    hipMemcpy(R, h.data(), nin * 4, hipMemcpyHostToDevice);
+  }
   for (int it = 0; it < 3; ++it)
     run();
   hipDeviceSynchronize();
@@ -55,9 +83,10 @@ int main(int argc, char** argv) {
   const char* names[12] = {"top barrier", "stage (split+lds)", "stage barrier", "mfma",
                            "epi barrier 1", "shear writes", "epi barrier 2", "store loop",
                            "stage: dma wait", "dma issue", "-", "-"};
-  if (h2) {
-    const char* hn[12] = {"barrier waits", "split+lds write", "load issue", "frags+mfma",
-                          "epilogue (shear, ring, stores)", "-", "-", "-", "-", "-", "-", "-"};
+  if (band) {
+    const char* hn[12] = {"barrier waits", "wait+stage (split, lds write)", "load+touch issue",
+                          "frags+mfma", "epilogue (shear, ring, stores)", "-", "-", "-", "-", "-",
+                          "-", "-"};
     double sm[12] = {0};
     int n = 0;
     for (int w = 0; w < 4096; ++w) {
@@ -69,7 +98,7 @@ int main(int argc, char** argv) {
     }
     double tt = 0;
     for (int p = 0; p < 12; ++p) tt += sm[p];
-    printf("kernel h2 %.1f us rc=%d, waves: %d, %.0f cycles/wave\n", ms * 1e3, rc, n, tt / (n ? n : 1));
+    printf("kernel %s %.1f us rc=%d, waves: %d, %.0f cycles/wave\n", mode, ms * 1e3, rc, n, tt / (n ? n : 1));
     for (int p = 0; p < 12; ++p)
       if (sm[p] > 0) printf("  %-30s %10.0f cycles/wave  %5.1f %%\n", hn[p], sm[p] / n, 100.0 * sm[p] / tt);
     return 0;

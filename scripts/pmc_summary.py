@@ -59,7 +59,7 @@ def main():
            "correction": "hbm_bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 (gfx950)",
            "kernels": {}}
     for k in sorted(set(fetch) & set(write)):
-        if "smcv" not in k and not k.startswith(("ip_", "softargmin", "argext", "dot_volume")):
+        if "smcv" not in k and not k.startswith(("ip_", "band_", "softargmin", "argext", "dot_volume")):
             continue
         fb, wb = 2 * fetch[k] * 1024, write[k] * 1024
         rec = {"fetch_bytes": fb, "write_bytes": wb, "hbm_bytes_per_launch": fb + wb}

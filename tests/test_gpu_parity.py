@@ -489,3 +489,99 @@ def test_cfg5_concat_interweave_fp16_full_size():
         assert torch.equal(sv[0, 0::2, d, :, d:], L[0, :16, :, d:])
         assert torch.equal(sv[0, 1::2, d, :, d:], R[0, :16, :, :960 - d])
         assert not sv[0, :, d, :, :d].any()
+
+
+# =============================================================================== band kernel: groupwise + fused
+GW_SHAPES = [(1, 32, 3, 260, 100, 4), (2, 48, 2, 132, 33, 3), (1, 64, 2, 512, 192, 8),
+             (1, 16, 2, 64, 256, 2), (1, 24, 2, 200, 40, 8), (1, 40, 2, 128, 7, 5)]
+
+
+@pytest.mark.parametrize("dt", ["f32", "f16", "bf16"])
+@pytest.mark.parametrize("shape", GW_SHAPES, ids=str)
+def test_groupwise_band_vs_oracle(shape, dt):
+    """The groupwise MFMA band kernel (D-innermost epilogue ring): fp32 (N,G,H,W,D) within 1e-4
+    of the fp64 oracle on the same dtype-rounded features -- channel tails (C/G not a multiple
+    of 16), two D passes, D % 4 != 0 (scalar d stores) and a partial last x tile."""
+    from realtime_stereo_matcher_amd import functional as F
+
+    n, c, h, w, D, G = shape
+    l, r = _feats(51, (n, c, h, w))
+    l, r = O.round_to_dtype(l, dt).astype(np.float32), O.round_to_dtype(r, dt).astype(np.float32)
+    got = F.groupwise_volume(dev(l, dt), dev(r, dt), G, D)
+    assert got.dtype == torch.float32 and got.shape == (n, G, h, w, D)
+    np.testing.assert_allclose(host(got), O.groupwise(l, r, G, D), atol=TOL, rtol=0)
+
+
+def test_groupwise_band_nonfinite():
+    """+-inf / NaN in one group's channels give inf / NaN only in that group's cells."""
+    from realtime_stereo_matcher_amd import functional as F
+
+    l, r = _feats(52, (1, 32, 3, 256))
+    l[0, 5, 0, 130] = np.inf   # group 0 (8 channels per group)
+    r[0, 19, 1, 100] = np.nan  # group 2
+    r[0, 30, 2, 3] = -np.inf   # group 3
+    got = host(F.groupwise_volume(dev(l), dev(r), 4, 48))
+    want = O.groupwise(l, r, 4, 48)
+    np.testing.assert_array_equal(np.isnan(got), np.isnan(want))
+    np.testing.assert_array_equal(np.isposinf(got), np.isposinf(want))
+    np.testing.assert_array_equal(np.isneginf(got), np.isneginf(want))
+    fin = np.isfinite(want)
+    np.testing.assert_allclose(got[fin], want[fin], atol=TOL, rtol=0)
+
+
+FUSED_SHAPES = [(1, 64, 3, 512, 192), (2, 20, 3, 260, 100), (1, 33, 2, 132, 31), (1, 16, 2, 64, 64),
+                (1, 8, 3, 100, 24), (1, 7, 2, 36, 40), (1, 16, 2, 64, 256), (1, 5, 2, 33, 9)]
+
+
+@pytest.mark.parametrize("mean", [False, True])
+@pytest.mark.parametrize("shape", FUSED_SHAPES, ids=str)
+def test_fused_soft_argmin(shape, mean):
+    """Volume + soft-argmin in one pass: the volume is bit-identical to the
+    volume op's, the disparity is the fp64 soft-argmin of that volume within 1e-4, and the
+    volume-free call returns the same disparity (D > 192 or W % 4 != 0: two kernels)."""
+    from realtime_stereo_matcher_amd import functional as F
+
+    n, c, h, w, D = shape
+    l, r = _feats(41, (n, c, h, w))
+    L, R = dev(l), dev(r)
+    vol, disp = F.inner_product_soft_argmin(L, R, D, mean=mean)
+    ref = F.correlation_volume(L, R, D) if mean else F.inner_product_volume(L, R, D)
+    assert torch.equal(vol, ref)
+    assert disp.shape == (n, 1, h, w) and disp.dtype == torch.float32
+    np.testing.assert_allclose(host(disp), O.softargmin(host(vol)), atol=TOL, rtol=0)
+    none, disp2 = F.inner_product_soft_argmin(L, R, D, mean=mean, keep_volume=False)
+    assert none is None and torch.equal(disp2, disp)
+
+
+def test_fused_soft_argmin_nonfinite_and_empty():
+    from realtime_stereo_matcher_amd import functional as F
+
+    l, r = _feats(23, (1, 16, 3, 256))
+    l[0, 5, 0, 130] = np.inf
+    l[0, 0, 1, 7] = -np.inf
+    r[0, 3, 1, 100] = np.nan
+    r[0, 9, 2, 3] = np.inf
+    vol, disp = F.inner_product_soft_argmin(dev(l), dev(r), 64)
+    v = host(vol)
+    np.testing.assert_array_equal(np.isnan(v), np.isnan(O.inner_product(l, r, 64)))
+    np.testing.assert_allclose(host(disp), O.softargmin(v), atol=TOL, rtol=0, equal_nan=True)
+    z = torch.zeros(1, 4, 2, 8, device="cuda")
+    vol0, disp0 = F.inner_product_soft_argmin(z, z, 0)
+    assert vol0.shape == (1, 0, 2, 8) and torch.equal(disp0, torch.zeros(1, 1, 2, 8, device="cuda"))
+
+
+def test_cfg2_fused_full_size():
+    """cfg2 through the fused kernel: the volume equals the volume op's bit for bit, the
+    disparity is the fp64 soft-argmin of that volume, with or without the volume written."""
+    from realtime_stereo_matcher_amd import functional as F
+
+    g = torch.Generator(device="cuda").manual_seed(0)
+    L = torch.randn(1, 64, 540, 960, device="cuda", generator=g)
+    R = torch.randn(1, 64, 540, 960, device="cuda", generator=g)
+    vol, disp = F.inner_product_soft_argmin(L, R, 192)
+    assert torch.equal(vol, F.inner_product_volume(L, R, 192))
+    _, disp2 = F.inner_product_soft_argmin(L, R, 192, keep_volume=False)
+    assert torch.equal(disp2, disp)
+    for y in (0, 1, 269, 539):
+        np.testing.assert_allclose(host(disp[:, :, y:y + 1]), O.softargmin(host(vol[:, :, y:y + 1])),
+                                   atol=TOL, rtol=0)
