@@ -144,6 +144,9 @@ __device__ __forceinline__ unsigned lds_addr(const void* p) {
 __device__ __forceinline__ void lds_store1(unsigned addr, float v) {
   *reinterpret_cast<__attribute__((address_space(3))) float*>(addr) = v;
 }
+__device__ __forceinline__ float lds_load1(unsigned addr) {
+  return *reinterpret_cast<__attribute__((address_space(3))) float*>(addr);
+}
 __device__ __forceinline__ f32x4v lds_load4(unsigned addr) {
   return *reinterpret_cast<__attribute__((address_space(3))) f32x4v*>(addr);
 }
@@ -305,8 +308,14 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
     st.nv = okp ? min(max(cpg - cl, 0), 8) : 0;
     // channel tail: clamp to the group's last channel (one code path; put() zeroes the tail)
     const int lim = cfull ? 7 : min(max(cpg - 1 - cl, 0), 7);
+    // the channel stride, opaque here: the 8 addresses are stepped, not 8 hoisted 64-bit offsets
+    int64_t csl = cs;
+    asm volatile("" : "+v"(csl));
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) gload<ASM>(st.v[kk], p + min(kk, lim) * cs);
+    for (int kk = 0; kk < 8; ++kk) {
+      gload<ASM>(st.v[kk], p);
+      if (kk < lim) p += csl;
+    }
   };
   // Touch every 128-B line a later step loads: lane (ch, g) loads one dword of channel
   // 8 ch + (g & 7) of its own pixel group -- the 8 groups of a line cover the line's 8
@@ -471,73 +480,57 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
   const int lane_st = LAYOUT == kNDHW ? rl * H * W + 4 * cl : rl * D + 4 * cl;
   const unsigned rdbase = LAYOUT == kNDHW ? ringw + (unsigned)(rl * 128 + 16 * cl)
                                           : ringw + (unsigned)(rl * 384 + 16 * cl);
+  const unsigned colbase = ringw + (unsigned)(16 * hh * 128 + 4 * lr);  // FUSE column reads
 
-  // fused soft-argmin state: pixels 4 cl + e of the wave, rows 8 qq + rl of every chunk
-  float fm[4];
-  double fs[4], ft[4];
-  int fnan = 0;
-  auto fuse_chunk = [&](int a, const f32x4v (&v)[4], int Dp, int rlo) {
-    // branch-free: selects only, so the block's code stays one basic block
+  // fused soft-argmin state: pixel lr of the wave, rows 16 hh .. 16 hh + 15 of every chunk (one
+  // pixel per lane: five registers of running state; the two row halves merge at the end)
+  float fm = -INFINITY;
+  double fs = 0.0, ft = 0.0;
+  bool fnan = false;
+  // chunk a's 16 rows of this lane's column, read back from the ring (conflict-free: the 32
+  // lanes of a half read consecutive words), folded into the online softmax
+  auto fuse_chunk = [&](int a, unsigned colb, int Dp, int hho) {
+    float vv[16];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float vv[4];
-#pragma unroll
-      for (int qq = 0; qq < 4; ++qq)  // beyond D: not in the softmax
-        vv[qq] = 32 * a + 8 * qq + rlo < Dp ? v[qq][e] : -INFINITY;
-      const bool nn = (vv[0] != vv[0]) | (vv[1] != vv[1]) | (vv[2] != vv[2]) | (vv[3] != vv[3]);
-      fnan |= nn ? (1 << e) : 0;
-      const float nm = fmaxf(fm[e], fmaxf(fmaxf(vv[0], vv[1]), fmaxf(vv[2], vv[3])));
-      const bool fin = nm != -INFINITY && nm != INFINITY;
-      // rescale the running sums to the new maximum (factor 1 when it did not grow)
-      const float f = fin && fm[e] != -INFINITY ? expf(fm[e] - nm) : 0.f;
-      float ps = 0.f, pt = 0.f;  // this chunk, disparities relative to its row 32 a + rl
-#pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        const float ex = fin ? expf(vv[qq] - nm) : 0.f;
-        ps += ex;
-        pt = fmaf((float)(8 * qq), ex, pt);
-      }
-      fs[e] = fs[e] * (double)f + (double)ps;
-      ft[e] = ft[e] * (double)f + (double)(32 * a + rlo) * (double)ps + (double)pt;
-      fm[e] = nm;
-      __builtin_amdgcn_sched_barrier(0);  // one pixel at a time: bounded temporaries
+    for (int r = 0; r < 16; ++r) {
+      const float x = lds_load1(colb + (unsigned)((a % 3) * kSlot + r * 128));
+      vv[r] = 32 * a + 16 * hho + r < Dp ? x : -INFINITY;  // beyond D: not in the softmax
     }
+    bool nn = false;
+    float cm = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      nn |= vv[r] != vv[r];
+      cm = fmaxf(cm, vv[r]);
+    }
+    fnan |= nn;
+    const float nm = fmaxf(fm, cm);
+    const bool fin = nm != -INFINITY && nm != INFINITY;
+    // rescale the running sums to the new maximum (factor 1 when it did not grow)
+    const float f = fin && fm != -INFINITY ? expf(fm - nm) : 0.f;
+    float ps = 0.f, pt = 0.f;  // this chunk, disparities relative to its row 32 a + 16 hh
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float ex = fin ? expf(vv[r] - nm) : 0.f;
+      ps += ex;
+      pt = fmaf((float)r, ex, pt);
+    }
+    fs = fs * (double)f + (double)ps;
+    ft = ft * (double)f + (double)(32 * a + 16 * hho) * (double)ps + (double)pt;
+    fm = nm;
   };
   auto fuse_finish = [&](const Work& k) {
-    fnan |= __shfl_xor(fnan, 8);
-    fnan |= __shfl_xor(fnan, 16);
-    fnan |= __shfl_xor(fnan, 32);
-    float dv[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float M = fm[e];
-      M = fmaxf(M, __shfl_xor(M, 8));
-      M = fmaxf(M, __shfl_xor(M, 16));
-      M = fmaxf(M, __shfl_xor(M, 32));
-      const double f =
-          (fm[e] == -INFINITY || M == INFINITY) ? 0.0 : (double)expf(fm[e] - M);
-      double s = fs[e] * f, t = ft[e] * f;
-      s += __shfl_xor(s, 8);
-      t += __shfl_xor(t, 8);
-      s += __shfl_xor(s, 16);
-      t += __shfl_xor(t, 16);
-      s += __shfl_xor(s, 32);
-      t += __shfl_xor(t, 32);
-      // NaN anywhere in the column, or an all -inf / any +inf column: NaN, as torch
-      dv[e] = (((fnan >> e) & 1) || M == INFINITY || M == -INFINITY) ? NAN : (float)(t / s);
-    }
-    if (rl == 0) {
-      const int x = k.x0 + 32 * wave + 4 * cl;
-      float* o = args.disp + ((size_t)k.n * H + k.y) * W + x;
-      if (x + 4 <= W) {
-        const f32x4v r = {dv[0], dv[1], dv[2], dv[3]};
-        store_quad<float>(o, r);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (x + e < W) store_one<float>(o + e, dv[e]);
-      }
-    }
+    const bool nn2 = __shfl_xor((int)fnan, 32) != 0;  // the other row half of the pixel
+    const float M = fmaxf(fm, __shfl_xor(fm, 32));
+    const double f = (fm == -INFINITY || M == INFINITY) ? 0.0 : (double)expf(fm - M);
+    double s = fs * f, t = ft * f;
+    s += __shfl_xor(s, 32);
+    t += __shfl_xor(t, 32);
+    // NaN anywhere in the column, or an all -inf / any +inf column: NaN, as torch
+    const bool bad = fnan || nn2 || M == INFINITY || M == -INFINITY;
+    const int x = k.x0 + 32 * wave + lr;
+    if (hh == 0 && x < W)
+      store_one<float>(args.disp + ((size_t)k.n * H + k.y) * W + x, bad ? NAN : (float)(t / s));
   };
 
   // SCALE: multiply back by 2^-(kL+kR); XLT: the segment has cells x < d (R pad rows), forced
@@ -548,13 +541,10 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
     const int kk = -(kL + kR);
     const int jlane = k.js + 32 * wave + 4 * hh;  // R row of element c_i of block 0, minus c_i
     if constexpr (FUSE) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        fm[e] = -INFINITY;
-        fs[e] = 0.0;
-        ft[e] = 0.0;
-      }
-      fnan = 0;
+      fm = -INFINITY;
+      fs = 0.0;
+      ft = 0.0;
+      fnan = false;
     }
 #pragma unroll
     for (int t = TMAX - 1; t >= 0; --t) {
@@ -562,9 +552,10 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
       // per block, opaque to the compiler: the per-element addresses and selects below are
       // recomputed in each block (two VALU each) instead of being hoisted out of the block loop
       // as 16+ loop-invariant registers (which spill at two workgroups per CU)
-      unsigned wb = wbase, rb = rdbase;
-      int uu = u, jl = jlane, ls_ = lane_st, rlo = rl, clo = cl;
+      unsigned wb = wbase, rb = rdbase, cb = colbase;
+      int uu = u, jl = jlane, ls_ = lane_st, rlo = rl, clo = cl, hho = hh;
       asm volatile("" : "+v"(wb), "+v"(uu), "+v"(jl), "+v"(rb), "+v"(ls_), "+v"(rlo), "+v"(clo));
+      if constexpr (FUSE) asm volatile("" : "+v"(cb), "+v"(hho));
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int ci = (i & 3) + 8 * (i >> 2);
@@ -600,7 +591,7 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
                                               : rb + (unsigned)(8 * qq * 384 + (a % 3) * 128);
           v[qq] = lds_load4(ra);
         }
-        if constexpr (FUSE) fuse_chunk(a, v, k.Dp, rlo);
+
         if (store_vol) {
           if constexpr (LAYOUT == kNDHW) {
             TO* ol = out + (((size_t)k.n * D + k.dp + 32 * a) * plane_stride +
@@ -647,6 +638,9 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
             }
           }
         }
+      }
+      if constexpr (FUSE) {
+        if (a >= 0) fuse_chunk(a, cb, k.Dp, hho);
       }
       // one block at a time (the live accumulators shrink block by block)
       __builtin_amdgcn_sched_barrier(0);
