@@ -9,7 +9,9 @@
 // a disparity plane is a coalesced 256 B / 1 KiB wave access; the four waves of a block split
 // D.  The softmax is a single streaming pass (online max with a rescale per 8-plane chunk)
 // with fp64 accumulators for sum(e) and sum(d*e): the result is within a few fp32 ulp of the
-// exact value, i.e. the parity error budget is torch's own fp32 noise.
+// exact value, i.e. the parity error budget is torch's own fp32 noise.  A plane whose rows are
+// contiguous is addressed as one flat pixel axis (no block straddles a row end), and fp32
+// soft-argmin there takes softargmin_f32x4_kernel (fp32 per chunk, fp64 across chunks).
 #include "common.h"
 
 #include <math.h>
@@ -21,7 +23,8 @@ constexpr int kThreads = 256;
 constexpr int kChunk = 8;
 
 struct VolView {
-  int64_t n, d, h;  // element strides; W stride is 1
+  int64_t n, d, h;    // element strides; W stride is 1
+  bool flat = false;  // rows contiguous: (H, W) is addressed as one axis of H*W pixels
 };
 
 // Block = 4 waves over the SAME 64*PX pixels of a row; wave w owns the disparity quarter
@@ -169,6 +172,127 @@ __global__ __launch_bounds__(kThreads) void softargmin_kernel(const T* __restric
   }
 }
 
+// fp32 soft-argmin over a volume whose (H, W) plane is contiguous, addressed as a flat pixel
+// axis (the host passes H = 1, W = H*W), so no block straddles a row end: cfg2's 518,400
+// pixels are exactly 2,025 blocks of 256, one round of the chip at 8 blocks per CU.
+// Same 4-wave disparity split as softargmin_kernel.  Per KC-plane chunk each lane folds its 4
+// pixels in fp32 (sum e and sum k*e relative to the chunk start, k < KC), and carries those
+// into fp64 sums once per chunk: 0.6 fp64 ops per element instead of 4, which is what kept
+// the fp64-per-element kernel compute-bound.  NaN and the +inf/-inf mix are caught by a
+// running fp32 sum of the raw values (NaN iff the column holds a NaN or both infinities).
+// FASTEXP: e = v_exp_f32((v - m) * log2 e); otherwise expf.
+template <int KC, bool FASTEXP>
+__global__ __launch_bounds__(kThreads) void softargmin_f32x4_kernel(const float* __restrict__ vol,
+                                                                    float* __restrict__ out,
+                                                                    int D, int W, int64_t vsn,
+                                                                    int64_t vsd) {
+  __shared__ float sm_m[3][4][64];
+  __shared__ float sm_p[3][4][64];
+  __shared__ double sm_s[3][4][64];
+  __shared__ double sm_t[3][4][64];
+  // unit = (n, 256-pixel group), n-major.  (Walking the units in the reverse of the order
+  // band_h2 writes them, so the freshest rows are read first, measured no faster at r01.)
+  const int P = (W + 255) >> 8;
+  const int unit = blockIdx.x;
+  const int n = unit / P;
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int x0 = ((unit - n * P) * 64 + lane) * 4;
+  const bool any = x0 < W;  // W % 4 == 0: a lane's 4 pixels are all in or all out
+  const int Dq = (D + 3) >> 2;
+  const int dbeg = min(D, wave * Dq);
+  const int dend = min(D, dbeg + Dq);
+  const float* base = vol + n * vsn + (any ? x0 : 0);
+  constexpr float kL2E = 1.4426950408889634f;
+
+  float m[4], probe[4];
+  double S[4], T[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    m[p] = -INFINITY;
+    probe[p] = 0.f;
+    S[p] = 0.0;
+    T[p] = 0.0;
+  }
+  if (any) {
+    for (int d0 = dbeg; d0 < dend; d0 += KC) {
+      const int nd = min(KC, dend - d0);
+      float4 v4[KC];
+#pragma unroll
+      for (int k = 0; k < KC; ++k)
+        v4[k] = *reinterpret_cast<const float4*>(base + (int64_t)min(d0 + k, dend - 1) * vsd);
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        float v[KC];
+#pragma unroll
+        for (int k = 0; k < KC; ++k) {
+          const float f = p == 0 ? v4[k].x : p == 1 ? v4[k].y : p == 2 ? v4[k].z : v4[k].w;
+          v[k] = (k < nd) ? f : -INFINITY;
+          if (k < nd) probe[p] += f;
+        }
+        float cm = v[0];
+#pragma unroll
+        for (int k = 1; k < KC; ++k) cm = fmaxf(cm, v[k]);
+        if (cm == -INFINITY) continue;  // nothing finite in this chunk (NaN: in probe)
+        if (cm > m[p]) {                 // new running max: rescale once per chunk
+          const double f = (m[p] == -INFINITY) ? 0.0 : (double)expf(m[p] - cm);
+          S[p] *= f;
+          T[p] *= f;
+          m[p] = cm;
+        }
+        float sc = 0.f, tc = 0.f;
+#pragma unroll
+        for (int k = 0; k < KC; ++k) {
+          const float e = FASTEXP ? __builtin_amdgcn_exp2f((v[k] - m[p]) * kL2E) : expf(v[k] - m[p]);
+          sc += e;
+          tc = fmaf((float)k, e, tc);
+        }
+        S[p] += (double)sc;
+        T[p] += (double)d0 * (double)sc + (double)tc;
+      }
+    }
+  }
+  if (wave != 0) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      sm_m[wave - 1][p][lane] = m[p];
+      sm_p[wave - 1][p][lane] = probe[p];
+      sm_s[wave - 1][p][lane] = S[p];
+      sm_t[wave - 1][p][lane] = T[p];
+    }
+  }
+  __syncthreads();
+  if (wave != 0 || !any) return;
+  float res[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    float M = m[p];
+    float pr = probe[p];
+    for (int w = 0; w < 3; ++w) {
+      M = fmaxf(M, sm_m[w][p][lane]);
+      pr += sm_p[w][p][lane];
+    }
+    double Sa = 0.0, Ta = 0.0;
+    if (M != -INFINITY && M != INFINITY) {
+      if (m[p] != -INFINITY) {
+        const double f = (double)expf(m[p] - M);
+        Sa = S[p] * f;
+        Ta = T[p] * f;
+      }
+      for (int w = 0; w < 3; ++w) {
+        const float mw = sm_m[w][p][lane];
+        if (mw == -INFINITY) continue;
+        const double f = (double)expf(mw - M);
+        Sa += sm_s[w][p][lane] * f;
+        Ta += sm_t[w][p][lane] * f;
+      }
+    }
+    // NaN anywhere in the column, an all -inf or any +inf column: NaN as in torch
+    res[p] = (D == 0) ? 0.f : (pr != pr || M == INFINITY || M == -INFINITY) ? NAN : (float)(Ta / Sa);
+  }
+  *reinterpret_cast<float4*>(out + (int64_t)n * W + x0) = make_float4(res[0], res[1], res[2], res[3]);
+}
+
 // Hard argmin/argmax with the same 4-wave disparity split; the quarters are merged in
 // disparity order with the same strict comparison, so the FIRST extreme index wins.
 template <typename T, bool MAXMODE>
@@ -251,7 +375,20 @@ int check_vol(const void* volume, const void* out, int dtype, int64_t N, int64_t
     vs->d = s[1];
     vs->h = s[2];
   }
+  // A plane whose rows are contiguous is one flat pixel axis: no block straddles a row end.
+  if (vs->h == W && H > 1 && H * W < ((int64_t)1 << 30)) {
+    vs->h = H * W;
+    vs->flat = true;
+  }
   return SM_OK;
+}
+
+// (H, W) -> (1, H*W) when check_vol flattened the plane (vs.h == H*W).
+inline void flatten_plane(const VolView& vs, int64_t* H, int64_t* W) {
+  if (vs.flat) {
+    *W = *H * *W;
+    *H = 1;
+  }
 }
 
 }  // namespace
@@ -266,6 +403,19 @@ int softargmin_entry(const void* volume, void* out, int dtype, int64_t N, int64_
   if (N * H * W == 0) return SM_OK;
   hipStream_t st = as_stream(stream);
   const bool presoft = flags == SM_REGRESS_PRESOFTMAXED;
+  flatten_plane(vs, &H, &W);
+  const bool flat4 = dtype == SM_F32 && !presoft && (H == 1) && (W % 4 == 0) &&
+                     (vs.d % 4 == 0) && (vs.n % 4 == 0) && (H * W < (int64_t)1 << 30) &&
+                     ((reinterpret_cast<uintptr_t>(volume) & 15u) == 0);
+  if (flat4) {
+    const int Wf = (int)W;
+    const int64_t nunits = ceil_div(Wf, 64 * 4) * N;
+    if (nunits > INT32_MAX) return fail(SM_EINVAL, "soft-argmin: too many pixels for one launch");
+    hipLaunchKernelGGL((softargmin_f32x4_kernel<8, true>), dim3((unsigned)nunits), dim3(kThreads),
+                       0, st, static_cast<const float*>(volume), static_cast<float*>(out), (int)D,
+                       Wf, vs.n, vs.d);
+    return check_launch("softargmin_f32x4_kernel");
+  }
   const bool v4 = dtype == SM_F32 && (W % 4 == 0) && (vs.h % 4 == 0) && (vs.d % 4 == 0) &&
                   (vs.n % 4 == 0) && ((reinterpret_cast<uintptr_t>(volume) & 15u) == 0);
   SM_DISPATCH_DTYPE(dtype, T, {
@@ -301,6 +451,7 @@ int argext_entry(const void* volume, int64_t* out, int dtype, int64_t N, int64_t
   if (N * H * W == 0) return SM_OK;
   if (D <= 0) return fail(SM_EINVAL, "argext over an empty D axis");
   hipStream_t st = as_stream(stream);
+  flatten_plane(vs, &H, &W);
   dim3 grid((unsigned)ceil_div(W, 64), (unsigned)H, (unsigned)N);
   SM_DISPATCH_DTYPE(dtype, T, {
     const T* v = static_cast<const T*>(volume);

@@ -374,6 +374,30 @@ def test_regression_special_values():
     np.testing.assert_array_equal(host(F.hard_argmin(dev(v))), torch.argmin(t, 1).numpy())
 
 
+@pytest.mark.parametrize("W", [8, 6])  # H*W % 4 == 0: the flat fp32 kernel; else the generic one
+def test_regression_special_values_flat(W):
+    """Special columns through the flat-plane fp32 soft-argmin (regress.hip), D = 37 so every
+    disparity quarter ends in a partial chunk."""
+    from realtime_stereo_matcher_amd import functional as F
+
+    D = 37
+    v = np.random.default_rng(4).standard_normal((2, D, 2, W)).astype(np.float32)
+    v[0, :, 0, 0] = -np.inf                      # all -inf -> NaN
+    v[0, :, 0, 1] = -np.inf
+    v[0, 12, 0, 1] = np.nan                      # NaN inside an all -inf chunk -> NaN
+    v[0, 3, 1, 1] = np.inf                       # +inf -> NaN
+    v[0, 30, 1, 2] = np.inf
+    v[0, 2, 1, 2] = -np.inf                      # +inf and -inf in one column -> NaN
+    v[1, :20, 1, 3] = -np.inf                    # leading -inf quarters, finite tail
+    v[1, 36, 0, 4] = 90.0                        # last disparity dominates
+    v[1, :, 1, 5] = np.linspace(-200, 200, D)    # steep ramp, rescales every chunk
+    t = torch.from_numpy(v)
+    ref = torch.sum(torch.softmax(t.double(), 1) * torch.arange(float(D)).view(1, -1, 1, 1), 1).float().numpy()
+    got = host(F.soft_argmin(dev(v), keepdim=False))
+    np.testing.assert_allclose(got, ref, atol=2e-5, equal_nan=True)
+    np.testing.assert_array_equal(np.isnan(got), np.isnan(ref))
+
+
 def test_zero_channels_and_empty():
     from realtime_stereo_matcher_amd import functional as F
 
