@@ -149,6 +149,18 @@ int sm_regress_argext(const void* volume, int64_t* out, int dtype,
                       int64_t N, int64_t D, int64_t H, int64_t W, int mode,
                       const int64_t* vol_strides, void* stream);
 
+/* §8f-4: warp an image / feature map by a disparity (1-channel) or flow (2-channel) map,
+ * replacing warp_by_flow_map (tools/warp.py:5-42; model/mobile_stereo_net_v2.py:59-96 and
+ * _v3.py:60-97, called by RefineNet _v3.py:136 / _v2.py:127): the reference's grid
+ * (x - fx, y - fy) normalised by (w - 1, h - 1), sampled by grid_sample bilinear, zero padding,
+ * align_corners=False.  image: (N, C, Hi, Wi); flow: (N, flow_channels, H, W) with
+ * flow_channels 1 or 2; out: (N, C, H, W) contiguous.  float32 only (SM_EDTYPE otherwise).
+ * Strides: element strides of (N, C, H, W) for image and flow (W stride 1; NULL = contiguous). */
+int sm_warp_by_flow(const void* image, const void* flow, void* out, int dtype,
+                    int64_t N, int64_t C, int64_t Hi, int64_t Wi, int64_t H, int64_t W,
+                    int64_t flow_channels, const int64_t* image_strides,
+                    const int64_t* flow_strides, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -36,6 +36,7 @@ SIGNATURES = {
     "sm_cv_diff": [_p, _p, _p, _i, _l, _l, _l, _l, _l, _lp, _lp, _p],
     "sm_regress_softargmin": [_p, _p, _i, _l, _l, _l, _l, _i, _lp, _p],
     "sm_regress_argext": [_p, _p, _i, _l, _l, _l, _l, _i, _lp, _p],
+    "sm_warp_by_flow": [_p, _p, _p, _i, _l, _l, _l, _l, _l, _l, _l, _lp, _lp, _p],
 }
 _RESTYPE = {"sm_last_error": ctypes.c_char_p}
 

@@ -39,6 +39,9 @@ int softargmin_entry(const void* volume, void* out, int dtype, int64_t N, int64_
                      int64_t W, int flags, const int64_t* vol_strides, void* stream);
 int argext_entry(const void* volume, int64_t* out, int dtype, int64_t N, int64_t D, int64_t H,
                  int64_t W, int mode, const int64_t* vol_strides, void* stream);
+int warp_entry(const void* image, const void* flow, void* out, int dtype, int64_t N, int64_t C,
+               int64_t Hi, int64_t Wi, int64_t H, int64_t W, int64_t flow_channels,
+               const int64_t* image_strides, const int64_t* flow_strides, void* stream);
 }  // namespace smcv
 
 using namespace smcv;
@@ -188,4 +191,13 @@ extern "C" int sm_regress_argext(const void* volume, int64_t* out, int dtype, in
                                  const int64_t* vol_strides, void* stream) {
   SM_ENTRY_BEGIN
   return argext_entry(volume, out, dtype, N, D, H, W, mode, vol_strides, stream);
+}
+
+extern "C" int sm_warp_by_flow(const void* image, const void* flow, void* out, int dtype,
+                               int64_t N, int64_t C, int64_t Hi, int64_t Wi, int64_t H, int64_t W,
+                               int64_t flow_channels, const int64_t* image_strides,
+                               const int64_t* flow_strides, void* stream) {
+  SM_ENTRY_BEGIN
+  return warp_entry(image, flow, out, dtype, N, C, Hi, Wi, H, W, flow_channels, image_strides,
+                    flow_strides, stream);
 }

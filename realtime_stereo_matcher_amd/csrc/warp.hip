@@ -1,0 +1,135 @@
+// Disparity / flow warp of an image or feature map.
+//
+//   warp_by_flow_map(image, flow)   tools/warp.py:5-42, model/mobile_stereo_net_v2.py:59-96
+//                                   (= _v3.py:60-97), called by RefineNet (_v3.py:136, _v2.py:127)
+//
+// The reference builds a sampling grid from the flow and calls F.grid_sample (bilinear, zero
+// padding, align_corners=False).  Its normalisation divides by (w - 1) and (h - 1) while
+// grid_sample un-normalises with align_corners=False, so the sampled position is
+//   ix = ((2 (x - fx) / (w - 1) - 1) + 1) * (Wi / 2) - 0.5,   and likewise iy with fy = 0 for a
+// one-channel flow: the warp also resamples vertically by h / (h - 1).  This kernel evaluates
+// exactly that fp32 operation sequence (the CPU grid_sample's form of the un-normalisation,
+// GridSamplerKernel.cpp: (g + 1) * size / 2 - 0.5) and the same bilinear weights
+// (nw = (1 - dy)(1 - dx), ...; out-of-image corners contribute 0, as zero padding).
+//
+// One lane owns one output pixel: it derives the four corner offsets and weights once, then
+// walks the channels, so each channel costs four gathers (neighbouring lanes read neighbouring
+// image pixels of at most two rows: L1/L2 hits) and one coalesced store.  The image is read
+// about once and the output written once: HBM-bound.
+#include "common.h"
+
+#include <math.h>
+
+namespace smcv {
+namespace {
+
+constexpr int kWarpThreads = 256;
+constexpr int kWarpCU = 4;  // channels in flight per lane
+
+struct WarpArgs {
+  const float* img;
+  const float* flow;
+  float* out;
+  int C, H, W, Hi, Wi, fch;
+  int64_t isn, isc, ish;  // image strides (W stride 1)
+  int64_t fsn, fsc, fsh;  // flow strides (W stride 1)
+  float sx, sy;           // Wi / 2, Hi / 2
+  float dw, dh;           // (float)(w - 1.0), (float)(h - 1.0)
+};
+
+__global__ __launch_bounds__(kWarpThreads) void warp_kernel(WarpArgs a) {
+#pragma clang fp contract(off)  // separate roundings, as the reference's grid math and blend
+  const int n = blockIdx.y;
+  const int64_t p = (int64_t)blockIdx.x * kWarpThreads + threadIdx.x;
+  const int64_t HW = (int64_t)a.H * a.W;
+  if (p >= HW) return;
+  const int y = (int)(p / a.W);
+  const int x = (int)(p - (int64_t)y * a.W);
+  const float* fl = a.flow + n * a.fsn + (int64_t)y * a.fsh + x;
+  // grid, exactly as the reference: (x - f) -> 2 * . / (w - 1) - 1   (tools/warp.py:19-36)
+  float gx = (float)x - fl[0];
+  float gy = (float)y;
+  if (a.fch == 2) gy = gy - fl[a.fsc];
+  gx = 2.0f * gx / a.dw - 1.0f;
+  gy = 2.0f * gy / a.dh - 1.0f;
+  // grid_sample, align_corners=False: un-normalise, bilinear corners
+  const float ix = (gx + 1.0f) * a.sx - 0.5f;
+  const float iy = (gy + 1.0f) * a.sy - 0.5f;
+  const float fx0 = floorf(ix), fy0 = floorf(iy);
+  const float dx = ix - fx0, dy = iy - fy0;
+  const float ex = 1.0f - dx, sy = 1.0f - dy;
+  float w[4] = {sy * ex, sy * dx, dy * ex, dy * dx};  // nw, ne, sw, se
+  int64_t off[4];
+  bool ok[4];
+  const bool finite = fabsf(ix) < 2.0e9f && fabsf(iy) < 2.0e9f;  // int conversion in range
+  const int x0 = finite ? (int)fx0 : -2, y0 = finite ? (int)fy0 : -2;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int xx = x0 + (k & 1), yy = y0 + (k >> 1);
+    ok[k] = finite && xx >= 0 && xx < a.Wi && yy >= 0 && yy < a.Hi;
+    off[k] = ok[k] ? (int64_t)yy * a.ish + xx : 0;
+  }
+  const float* ib = a.img + n * a.isn;
+  float* ob = a.out + ((int64_t)n * a.C) * HW + p;
+  int c = 0;
+  for (; c + kWarpCU <= a.C; c += kWarpCU) {
+    float v[kWarpCU][4];
+#pragma unroll
+    for (int u = 0; u < kWarpCU; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[u][k] = ok[k] ? ib[(int64_t)(c + u) * a.isc + off[k]] : 0.f;
+#pragma unroll
+    for (int u = 0; u < kWarpCU; ++u)
+      ob[(int64_t)(c + u) * HW] = v[u][0] * w[0] + v[u][1] * w[1] + v[u][2] * w[2] + v[u][3] * w[3];
+  }
+  for (; c < a.C; ++c) {
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = ok[k] ? ib[(int64_t)c * a.isc + off[k]] : 0.f;
+    ob[(int64_t)c * HW] = v[0] * w[0] + v[1] * w[1] + v[2] * w[2] + v[3] * w[3];
+  }
+}
+
+}  // namespace
+
+int warp_entry(const void* image, const void* flow, void* out, int dtype, int64_t N, int64_t C,
+               int64_t Hi, int64_t Wi, int64_t H, int64_t W, int64_t flow_channels,
+               const int64_t* image_strides, const int64_t* flow_strides, void* stream) {
+  if (dtype != SM_F32) return fail(SM_EDTYPE, "warp_by_flow_map: float32 image and flow only");
+  if (N < 0 || C < 0 || Hi < 0 || Wi < 0 || H < 0 || W < 0) return fail(SM_EINVAL, "negative size");
+  if (flow_channels != 1 && flow_channels != 2)
+    return fail(SM_EINVAL, "invalid flow map dimension (1 or 2)");
+  if (N > 65535) return fail(SM_EINVAL, "N > 65535 not supported");
+  if (H * W >= ((int64_t)1 << 31) || Hi >= INT32_MAX || Wi >= INT32_MAX || C >= INT32_MAX)
+    return fail(SM_EINVAL, "warp_by_flow_map: plane too large");
+  if (N * C * H * W == 0) return SM_OK;
+  if (image == nullptr || flow == nullptr || out == nullptr) return fail(SM_EINVAL, "null pointer");
+  WarpArgs a;
+  a.img = static_cast<const float*>(image);
+  a.flow = static_cast<const float*>(flow);
+  a.out = static_cast<float*>(out);
+  a.C = (int)C, a.H = (int)H, a.W = (int)W, a.Hi = (int)Hi, a.Wi = (int)Wi;
+  a.fch = (int)flow_channels;
+  if (image_strides) {
+    if (image_strides[3] != 1 && Wi > 1) return fail(SM_EINVAL, "image: W stride must be 1");
+    a.isn = image_strides[0], a.isc = image_strides[1], a.ish = image_strides[2];
+  } else {
+    a.ish = Wi, a.isc = Hi * Wi, a.isn = C * Hi * Wi;
+  }
+  if (flow_strides) {
+    if (flow_strides[3] != 1 && W > 1) return fail(SM_EINVAL, "flow: W stride must be 1");
+    a.fsn = flow_strides[0], a.fsc = flow_strides[1], a.fsh = flow_strides[2];
+  } else {
+    a.fsh = W, a.fsc = H * W, a.fsn = flow_channels * H * W;
+  }
+  // the reference's scalars: (w - 1.0), (h - 1.0) rounded to the grid dtype; Wi / 2, Hi / 2
+  a.dw = (float)((double)W - 1.0);
+  a.dh = (float)((double)H - 1.0);
+  a.sx = (float)Wi / 2.0f;
+  a.sy = (float)Hi / 2.0f;
+  dim3 grid((unsigned)ceil_div(H * W, kWarpThreads), (unsigned)N);
+  hipLaunchKernelGGL(warp_kernel, grid, dim3(kWarpThreads), 0, as_stream(stream), a);
+  return check_launch("warp_kernel");
+}
+
+}  // namespace smcv

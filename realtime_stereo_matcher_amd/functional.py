@@ -17,6 +17,7 @@ Reference operators mirrored (babiking/realtime_stereo_matcher):
   soft_argmin            model/mobile_disp_net_c.py:208-220, model/mobile_stereo_net.py:144-147
   regression_presoftmax  model/mobile_stereo_net_v4.py:10-14
   hard_argmin/argmax     build-defined
+  warp_by_flow_map       tools/warp.py:5-42, model/mobile_stereo_net_v2.py:59-96
 """
 from __future__ import annotations
 
@@ -353,3 +354,38 @@ def hard_argmin(volume):
 def hard_argmax(volume):
     """First index of the maximum over D -> (N,H,W) int64 (ties -> lowest d, NaN wins)."""
     return _argext(volume, _lib.SM_ARGMAX, "hard_argmax")
+
+
+# ------------------------------------------------------------------------------ §8f-4 warp
+def warp_by_flow_map(image, flow):
+    """Warp ``image`` (N,C,Hi,Wi) by a disparity / flow map ``flow`` (N,1|2,H,W) -> (N,C,H,W).
+
+    Mirrors ``warp_by_flow_map`` (tools/warp.py:5-42, model/mobile_stereo_net_v2.py:59-96,
+    _v3.py:60-97): grid (x - fx, y - fy) normalised by (w - 1, h - 1), bilinear grid_sample with
+    zero padding and align_corners=False, evaluated by ONE HIP kernel (csrc/warp.hip).
+    float32 only; the same AssertionError as the reference for a flow with 3+ channels.
+    """
+    if not isinstance(image, torch.Tensor) or not isinstance(flow, torch.Tensor):
+        raise TypeError("warp_by_flow_map: image and flow must be tensors")
+    if flow.dim() != 4:
+        raise ValueError(f"warp_by_flow_map: expected a 4-D flow map, got {tuple(flow.shape)}")
+    n, c, h, w = flow.shape
+    assert c == 1 or c == 2, f"invalid flow map dimension 1 or 2 ({c})!"  # tools/warp.py:18
+    if image.dim() != 4:
+        raise RuntimeError(f"warp_by_flow_map: expected a 4-D image, got {tuple(image.shape)}")
+    if image.shape[0] != n:
+        raise RuntimeError(f"warp_by_flow_map: image batch {image.shape[0]} != flow batch {n}")
+    if image.dtype != torch.float32 or flow.dtype != torch.float32:
+        raise TypeError(f"warp_by_flow_map: float32 image and flow only (got {image.dtype}, "
+                        f"{flow.dtype})")
+    dev = _device_check(image, flow)
+    image = _stride_ok(_rows_contiguous(image))
+    flow = _stride_ok(_rows_contiguous(flow))
+    N, C, Hi, Wi = image.shape
+    out = torch.empty((N, C, h, w), dtype=image.dtype, device=dev)
+    if out.numel():
+        lib = _lib.load()
+        _lib.check(lib.sm_warp_by_flow(_ptr(image), _ptr(flow), _ptr(out), _lib.SM_F32, N, C, Hi,
+                                       Wi, h, w, c, _lib.strides_arg(image),
+                                       _lib.strides_arg(flow), _stream(dev)), "sm_warp_by_flow")
+    return out

@@ -111,6 +111,17 @@ def main():
     L, R = feats((1, 32, 68, 120), torch.float32)
     run("diff_volume_f32_model", lambda: F.difference_volume(L, R, 24),
         2 * L.numel() * 4 + 32 * 24 * 68 * 120 * 4)
+    del L, R
+
+    # §8f-4 warp: 1x32x540x960 fp32 features by a 0..192 disparity map (read image + flow,
+    # write the warped map once)
+    img, _ = feats((1, 32, 540, 960), torch.float32)
+    disp = torch.rand(1, 1, 540, 960, device="cuda") * 192
+    run("warp_disp_f32_540x960x32", lambda: F.warp_by_flow_map(img, disp),
+        2 * img.numel() * 4 + disp.numel() * 4)
+    flow2 = torch.randn(1, 2, 540, 960, device="cuda") * 4
+    run("warp_flow2_f32_540x960x32", lambda: F.warp_by_flow_map(img, flow2),
+        2 * img.numel() * 4 + flow2.numel() * 4)
 
 
 if __name__ == "__main__":

@@ -18,6 +18,7 @@ Reference call sites exercised (file:line under /root/reference):
   * interweave_tensors        model/mobile_stereo_net_v4.py:17-23 (+ shifted use :443-461)
   * inline soft-argmin        model/mobile_stereo_net.py:144-147
   * hard argmin/argmax        build-defined (torch.argmax/argmin over the reference volume)
+  * warp_by_flow_map          tools/warp.py:5-42
 
 Usage:  cd /root/repo && python3 -B tests/golden/gen_golden.py
 """
@@ -48,6 +49,7 @@ iw_mod = _load("cost_volume/interweave.py", "ref_interweave")
 msn_mod = _load("model/mobile_stereo_net.py", "ref_msn")
 v4_mod = _load("model/mobile_stereo_net_v4.py", "ref_msn_v4")
 dnc_mod = _load("model/mobile_disp_net_c.py", "ref_dispnetc")
+warp_mod = _load("tools/warp.py", "ref_warp")
 
 DT = {"f32": torch.float32, "f16": torch.float16, "bf16": torch.bfloat16}
 
@@ -223,6 +225,25 @@ def main():
         dv = msn_mod.make_cost_volume(L, R, 12).abs().sum(dim=1)  # SAD-style cost (N,D,H,W)
         save(f"argmin_{kind}_n2c8h5w33_d12_f32", "argext", {"max_disparity": 12, "mode": "min"},
              {"volume": dv, "out": torch.argmin(dv, dim=1)}, "f32", exact=True)
+
+    # ---------------- §8f-4 warp_by_flow_map (tools/warp.py:5-42) -------------
+    rng = np.random.default_rng(90)
+    warp_cases = [  # name, image shape, flow shape, flow generator
+        ("disp_n1c3h12w40", (1, 3, 12, 40), (1, 1, 12, 40), lambda sh: rng.uniform(0, 20, sh)),
+        ("flow2_n2c5h9w17", (2, 5, 9, 17), (2, 2, 9, 17), lambda sh: rng.standard_normal(sh) * 3),
+        ("resize_n1c4h6w20_to_h12w40", (1, 4, 6, 20), (1, 1, 12, 40), lambda sh: rng.uniform(-5, 45, sh)),
+        ("disp_n1c32h30w40", (1, 32, 30, 40), (1, 1, 30, 40), lambda sh: rng.uniform(0, 24, sh)),
+        ("intdisp_n1c6h8w33", (1, 6, 8, 33), (1, 1, 8, 33), lambda sh: rng.integers(0, 12, sh)),
+    ]
+    for name, ish, fsh, gen in warp_cases:
+        img = torch.from_numpy(rng.standard_normal(ish).astype(np.float32))
+        flow = torch.from_numpy(np.asarray(gen(fsh), dtype=np.float32))
+        out = warp_mod.warp_by_flow_map(img, flow)
+        save(f"warp_{name}_f32", "warp", {}, {"image": img, "flow": flow, "out": out}, "f32")
+    try:
+        warp_mod.warp_by_flow_map(torch.zeros(1, 2, 3, 4), torch.zeros(1, 3, 3, 4))
+    except AssertionError as e:
+        manifest["warp_assert_message_c3"] = str(e)
 
     # shape-mismatch behaviour of the reference (RuntimeError from torch)
     try:

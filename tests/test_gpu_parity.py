@@ -609,3 +609,60 @@ def test_cfg2_fused_full_size():
     for y in (0, 1, 269, 539):
         np.testing.assert_allclose(host(disp[:, :, y:y + 1]), O.softargmin(host(vol[:, :, y:y + 1])),
                                    atol=TOL, rtol=0)
+
+
+# ================================================================================ §8f-4 warp
+@pytest.mark.parametrize("rec", cases("warp"), ids=_ids(cases("warp")))
+def test_golden_warp(rec):
+    from realtime_stereo_matcher_amd.tools.warp import warp_by_flow_map
+
+    a = load_case(rec)
+    out = warp_by_flow_map(dev(a["image"]), dev(a["flow"]))
+    assert out.shape == a["out"].shape and out.dtype == torch.float32
+    np.testing.assert_allclose(host(out), a["out"], atol=TOL, rtol=0)
+
+
+@pytest.mark.parametrize("ish,fsh", [((2, 7, 33, 65), (2, 1, 33, 65)), ((1, 3, 17, 30), (1, 2, 40, 61)),
+                                     ((1, 5, 1, 9), (1, 1, 2, 9)), ((3, 1, 8, 8), (3, 2, 8, 8))])
+def test_warp_vs_oracle(ish, fsh):
+    from realtime_stereo_matcher_amd.functional import warp_by_flow_map
+
+    rng = np.random.default_rng(11)
+    img = rng.standard_normal(ish).astype(np.float32)
+    flow = (rng.standard_normal(fsh) * 8 + 4).astype(np.float32)
+    flow[..., 0, :3] = 1e9       # far outside: all corners padded -> 0
+    flow[..., -1, -2:] = -3.0    # exact integer shift
+    np.testing.assert_allclose(host(warp_by_flow_map(dev(img), dev(flow))),
+                               O.warp_by_flow_map(img, flow), atol=TOL, rtol=0)
+
+
+def test_warp_strided_and_errors():
+    from realtime_stereo_matcher_amd.functional import warp_by_flow_map
+
+    rng = np.random.default_rng(12)
+    img = rng.standard_normal((2, 6, 10, 24)).astype(np.float32)
+    flow = rng.uniform(0, 6, (2, 2, 10, 24)).astype(np.float32)
+    I, Fl = dev(img), dev(flow)
+    got = warp_by_flow_map(I[:, ::2], Fl[:, :1])         # channel-strided image, 1-ch flow view
+    np.testing.assert_allclose(host(got), O.warp_by_flow_map(img[:, ::2], flow[:, :1]), atol=TOL, rtol=0)
+    assert warp_by_flow_map(I[:, :0], Fl[:, :1]).shape == (2, 0, 10, 24)
+    with pytest.raises(AssertionError, match="invalid flow map dimension"):
+        warp_by_flow_map(I, torch.zeros(2, 3, 10, 24, device="cuda"))
+    with pytest.raises(TypeError):
+        warp_by_flow_map(I.half(), Fl[:, :1].half())
+    with pytest.raises(RuntimeError):
+        warp_by_flow_map(I.cpu(), Fl[:, :1].cpu())
+
+
+def test_warp_full_size_rows():
+    """1x32x540x960 features warped by a 0..192 disparity map (RefineNet-style, full KITTI
+    quarter-res plane): sampled rows, the border rows included, against the oracle."""
+    from realtime_stereo_matcher_amd.functional import warp_by_flow_map
+
+    g = torch.Generator(device="cuda").manual_seed(5)
+    I = torch.randn(1, 32, 540, 960, device="cuda", generator=g)
+    Fl = torch.rand(1, 1, 540, 960, device="cuda", generator=g) * 192
+    out = warp_by_flow_map(I, Fl)
+    rows = [0, 1, 269, 538, 539]
+    ref = O.warp_by_flow_map(host(I), host(Fl), rows=rows)
+    np.testing.assert_allclose(host(out[:, :, rows]), ref, atol=TOL, rtol=0)

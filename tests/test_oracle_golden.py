@@ -148,3 +148,18 @@ def test_torch_port_correlation(rec):
 def test_torch_port_softargmin(rec):
     a = load_case(rec)
     np.testing.assert_array_equal(P.soft_argmin_eager(torch.from_numpy(a["volume"])).numpy(), a["out"])
+
+
+# ------------------------------------------------------------------------------ §8f-4 warp
+@pytest.mark.parametrize("rec", cases("warp"), ids=_ids(cases("warp")))
+def test_warp(rec):
+    a = load_case(rec)
+    got = O.warp_by_flow_map(a["image"], a["flow"])
+    assert got.shape == a["out"].shape and got.dtype == np.float32
+    np.testing.assert_allclose(got, a["out"], atol=TOL_F32, rtol=0)
+
+
+def test_warp_assert_message(manifest):
+    with pytest.raises(AssertionError) as e:
+        O.warp_by_flow_map(np.zeros((1, 2, 3, 4), np.float32), np.zeros((1, 3, 3, 4), np.float32))
+    assert str(e.value) == manifest["warp_assert_message_c3"]
