@@ -20,6 +20,8 @@
 
 #include <math.h>
 
+#include <algorithm>
+
 namespace smcv {
 namespace {
 
@@ -90,6 +92,83 @@ __global__ __launch_bounds__(kWarpThreads) void warp_kernel(WarpArgs a) {
   }
 }
 
+// Disparity (one-channel flow) warps: iy does not depend on x, so output row y reads only
+// image rows y0 = floor(iy) and y0 + 1.  A block owns (n, y, a chunk of CC channels): it copies
+// those two rows of its channels into LDS with coalesced 16-B loads (column 0 is a zero pad
+// that out-of-image corners read), then every lane blends its pixels from LDS: the random
+// per-lane x of a disparity map costs LDS bank conflicts instead of one L1 request per lane.
+// Same operation sequence (and results) as warp_kernel.
+template <bool V4>
+__global__ __launch_bounds__(kWarpThreads) void warp_rows_kernel(WarpArgs a, int CC) {
+#pragma clang fp contract(off)
+  extern __shared__ float srow[];  // [CC][2][Wi + 4]: element 3 of each row is the zero pad
+  const int c0 = blockIdx.x * CC;
+  const int y = blockIdx.y;
+  const int n = blockIdx.z;
+  const int nc = min(CC, a.C - c0);
+  const int RS = a.Wi + 4;  // row stride in LDS (16-B aligned rows, data from element 4)
+  const float gy = 2.0f * (float)y / a.dh - 1.0f;
+  const float iy = (gy + 1.0f) * a.sy - 0.5f;
+  const float fy0 = floorf(iy);
+  const float dy = iy - fy0, sy = 1.0f - dy;
+  const bool finite = fabsf(iy) < 2.0e9f;
+  const int y0 = finite ? (int)fy0 : -2;
+  // ---- stage rows y0, y0 + 1 of channels c0 .. c0 + nc (all loads of a lane issued first)
+  const float* ib = a.img + n * a.isn + (int64_t)c0 * a.isc;
+  const bool r0ok = y0 >= 0 && y0 < a.Hi, r1ok = y0 + 1 >= 0 && y0 + 1 < a.Hi;
+  const int64_t roff0 = (int64_t)(r0ok ? y0 : 0) * a.ish, roff1 = (int64_t)(r1ok ? y0 + 1 : 0) * a.ish;
+  if (threadIdx.x < 2 * nc) srow[threadIdx.x * RS + 3] = 0.f;
+  if (V4) {
+    const int Q = a.Wi >> 2, total = 2 * nc * Q;
+    constexpr int U = 8;
+    for (int i0 = threadIdx.x; i0 < total; i0 += U * kWarpThreads) {
+      float4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * kWarpThreads;
+        const int r = i / Q, q = i - r * Q;
+        const bool ok = i < total && ((r & 1) ? r1ok : r0ok);
+        v[u] = ok ? reinterpret_cast<const float4*>(ib + (int64_t)(r >> 1) * a.isc + ((r & 1) ? roff1 : roff0))[q]
+                  : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * kWarpThreads;
+        const int r = i / Q, q = i - r * Q;
+        if (i < total) reinterpret_cast<float4*>(srow + r * RS + 4)[q] = v[u];
+      }
+    }
+  } else {
+    const int total = 2 * nc * a.Wi;
+    for (int i = threadIdx.x; i < total; i += kWarpThreads) {
+      const int r = i / a.Wi, q = i - r * a.Wi;
+      const bool ok = (r & 1) ? r1ok : r0ok;
+      srow[r * RS + 4 + q] = ok ? ib[(int64_t)(r >> 1) * a.isc + ((r & 1) ? roff1 : roff0) + q] : 0.f;
+    }
+  }
+  __syncthreads();
+  const int64_t HW = (int64_t)a.H * a.W;
+  float* ob = a.out + ((int64_t)n * a.C + c0) * HW + (int64_t)y * a.W;
+  const float* fl = a.flow + n * a.fsn + (int64_t)y * a.fsh;
+  for (int x = threadIdx.x; x < a.W; x += kWarpThreads) {
+    float gx = (float)x - fl[x];
+    gx = 2.0f * gx / a.dw - 1.0f;
+    const float ix = (gx + 1.0f) * a.sx - 0.5f;
+    const float fx0 = floorf(ix);
+    const float dx = ix - fx0, ex = 1.0f - dx;
+    const float w0 = sy * ex, w1 = sy * dx, w2 = dy * ex, w3 = dy * dx;  // nw, ne, sw, se
+    const bool ok = finite && fabsf(ix) < 2.0e9f;
+    const int x0 = ok ? (int)fx0 : -2;
+    const int ia = (ok && x0 >= 0 && x0 < a.Wi) ? x0 + 4 : 3;
+    const int ib2 = (ok && x0 + 1 >= 0 && x0 + 1 < a.Wi) ? x0 + 5 : 3;
+    for (int c = 0; c < nc; ++c) {
+      const float* s0 = srow + (2 * c) * RS;
+      const float* s1 = s0 + RS;
+      ob[(int64_t)c * HW + x] = s0[ia] * w0 + s0[ib2] * w1 + s1[ia] * w2 + s1[ib2] * w3;
+    }
+  }
+}
+
 }  // namespace
 
 int warp_entry(const void* image, const void* flow, void* out, int dtype, int64_t N, int64_t C,
@@ -127,8 +206,24 @@ int warp_entry(const void* image, const void* flow, void* out, int dtype, int64_
   a.dh = (float)((double)H - 1.0);
   a.sx = (float)Wi / 2.0f;
   a.sy = (float)Hi / 2.0f;
+  hipStream_t st = as_stream(stream);
+  // disparity warps with rows that fit: the LDS row kernel, CC channels per block (<= 32 KB)
+  const int64_t row_bytes = 2 * (Wi + 4) * 4;
+  if (flow_channels == 1 && row_bytes <= 32768 && H <= 65535) {
+    // CC = 4 at Wi = 960 (measured r01: CC 1/2/4/8 -> 70/48/42/58 us on 1x32x540x960)
+    const int CC = (int)std::max<int64_t>(1, std::min<int64_t>(8, 32768 / row_bytes));
+    const bool v4 = (Wi % 4 == 0) && (a.ish % 4 == 0) && (a.isc % 4 == 0) && (a.isn % 4 == 0) &&
+                    ((reinterpret_cast<uintptr_t>(image) & 15u) == 0);
+    dim3 grid((unsigned)ceil_div(C, CC), (unsigned)H, (unsigned)N);
+    const size_t shm = (size_t)CC * row_bytes;
+    if (v4)
+      hipLaunchKernelGGL(warp_rows_kernel<true>, grid, dim3(kWarpThreads), shm, st, a, CC);
+    else
+      hipLaunchKernelGGL(warp_rows_kernel<false>, grid, dim3(kWarpThreads), shm, st, a, CC);
+    return check_launch("warp_rows_kernel");
+  }
   dim3 grid((unsigned)ceil_div(H * W, kWarpThreads), (unsigned)N);
-  hipLaunchKernelGGL(warp_kernel, grid, dim3(kWarpThreads), 0, as_stream(stream), a);
+  hipLaunchKernelGGL(warp_kernel, grid, dim3(kWarpThreads), 0, st, a);
   return check_launch("warp_kernel");
 }
 

@@ -119,6 +119,10 @@ def main():
     disp = torch.rand(1, 1, 540, 960, device="cuda") * 192
     run("warp_disp_f32_540x960x32", lambda: F.warp_by_flow_map(img, disp),
         2 * img.numel() * 4 + disp.numel() * 4)
+    ramp = torch.linspace(0, 192, 960, device="cuda").view(1, 1, 1, 960).expand(1, 1, 540, 960)
+    smooth = (ramp + torch.rand(1, 1, 540, 960, device="cuda")).contiguous()  # slanted plane
+    run("warp_smooth_disp_f32_540x960x32", lambda: F.warp_by_flow_map(img, smooth),
+        2 * img.numel() * 4 + smooth.numel() * 4)
     flow2 = torch.randn(1, 2, 540, 960, device="cuda") * 4
     run("warp_flow2_f32_540x960x32", lambda: F.warp_by_flow_map(img, flow2),
         2 * img.numel() * 4 + flow2.numel() * 4)
