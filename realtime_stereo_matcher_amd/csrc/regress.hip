@@ -172,22 +172,56 @@ __global__ __launch_bounds__(kThreads) void softargmin_kernel(const T* __restric
   }
 }
 
+// One KC-plane chunk of a lane's pixel p into its online-softmax state (m, S, T).  FULL: all KC
+// planes are real (no per-element masking).  NaN handling: a NaN in a chunk that has a finite
+// value makes e, hence S, NaN; a chunk with nothing but -inf and NaN poisons the pixel with
+// m = +inf, which the merge turns into NaN like a +inf column (torch gives NaN for both).
+template <int KC, bool FULL>
+__device__ __forceinline__ void fold_chunk(const float (&v)[KC], int nd, int d0, float& m,
+                                           double& S, double& T) {
+  constexpr float kL2E = 1.4426950408889634f;
+  float cm = FULL || 0 < nd ? v[0] : -INFINITY;
+#pragma unroll
+  for (int k = 1; k < KC; ++k) cm = fmaxf(cm, (FULL || k < nd) ? v[k] : -INFINITY);
+  if (cm == -INFINITY) {  // nothing finite: only a NaN matters
+    bool nan = false;
+#pragma unroll
+    for (int k = 0; k < KC; ++k) nan |= (FULL || k < nd) && v[k] != v[k];
+    if (nan) m = INFINITY;
+    return;
+  }
+  if (cm > m) {  // new running max: rescale once per chunk
+    const double f = (m == -INFINITY) ? 0.0 : (double)expf(m - cm);
+    S *= f;
+    T *= f;
+    m = cm;
+  }
+  float sc = 0.f, tc = 0.f;
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    if (FULL || k < nd) {
+      const float e = __builtin_amdgcn_exp2f((v[k] - m) * kL2E);
+      sc += e;
+      tc = fmaf((float)k, e, tc);
+    }
+  }
+  S += (double)sc;
+  T += (double)d0 * (double)sc + (double)tc;
+}
+
 // fp32 soft-argmin over a volume whose (H, W) plane is contiguous, addressed as a flat pixel
 // axis (the host passes H = 1, W = H*W), so no block straddles a row end: cfg2's 518,400
-// pixels are exactly 2,025 blocks of 256, one round of the chip at 8 blocks per CU.
+// pixels are exactly 2,025 blocks of 256.
 // Same 4-wave disparity split as softargmin_kernel.  Per KC-plane chunk each lane folds its 4
-// pixels in fp32 (sum e and sum k*e relative to the chunk start, k < KC), and carries those
-// into fp64 sums once per chunk: 0.6 fp64 ops per element instead of 4, which is what kept
-// the fp64-per-element kernel compute-bound.  NaN and the +inf/-inf mix are caught by a
-// running fp32 sum of the raw values (NaN iff the column holds a NaN or both infinities).
-// FASTEXP: e = v_exp_f32((v - m) * log2 e); otherwise expf.
-template <int KC, bool FASTEXP>
+// pixels in fp32 (sum e and sum k*e relative to the chunk start, k < KC, e = 2^((v-m) log2 e)
+// on v_exp_f32), and carries those into fp64 sums once per chunk: 0.6 fp64 ops per element
+// instead of 4, which is what kept the fp64-per-element kernel compute-bound.
+template <int KC>
 __global__ __launch_bounds__(kThreads) void softargmin_f32x4_kernel(const float* __restrict__ vol,
                                                                     float* __restrict__ out,
                                                                     int D, int W, int64_t vsn,
                                                                     int64_t vsd) {
   __shared__ float sm_m[3][4][64];
-  __shared__ float sm_p[3][4][64];
   __shared__ double sm_s[3][4][64];
   __shared__ double sm_t[3][4][64];
   // unit = (n, 256-pixel group), n-major.  (Walking the units in the reverse of the order
@@ -203,14 +237,12 @@ __global__ __launch_bounds__(kThreads) void softargmin_f32x4_kernel(const float*
   const int dbeg = min(D, wave * Dq);
   const int dend = min(D, dbeg + Dq);
   const float* base = vol + n * vsn + (any ? x0 : 0);
-  constexpr float kL2E = 1.4426950408889634f;
 
-  float m[4], probe[4];
+  float m[4];
   double S[4], T[4];
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     m[p] = -INFINITY;
-    probe[p] = 0.f;
     S[p] = 0.0;
     T[p] = 0.0;
   }
@@ -225,30 +257,12 @@ __global__ __launch_bounds__(kThreads) void softargmin_f32x4_kernel(const float*
       for (int p = 0; p < 4; ++p) {
         float v[KC];
 #pragma unroll
-        for (int k = 0; k < KC; ++k) {
-          const float f = p == 0 ? v4[k].x : p == 1 ? v4[k].y : p == 2 ? v4[k].z : v4[k].w;
-          v[k] = (k < nd) ? f : -INFINITY;
-          if (k < nd) probe[p] += f;
-        }
-        float cm = v[0];
-#pragma unroll
-        for (int k = 1; k < KC; ++k) cm = fmaxf(cm, v[k]);
-        if (cm == -INFINITY) continue;  // nothing finite in this chunk (NaN: in probe)
-        if (cm > m[p]) {                 // new running max: rescale once per chunk
-          const double f = (m[p] == -INFINITY) ? 0.0 : (double)expf(m[p] - cm);
-          S[p] *= f;
-          T[p] *= f;
-          m[p] = cm;
-        }
-        float sc = 0.f, tc = 0.f;
-#pragma unroll
-        for (int k = 0; k < KC; ++k) {
-          const float e = FASTEXP ? __builtin_amdgcn_exp2f((v[k] - m[p]) * kL2E) : expf(v[k] - m[p]);
-          sc += e;
-          tc = fmaf((float)k, e, tc);
-        }
-        S[p] += (double)sc;
-        T[p] += (double)d0 * (double)sc + (double)tc;
+        for (int k = 0; k < KC; ++k)
+          v[k] = p == 0 ? v4[k].x : p == 1 ? v4[k].y : p == 2 ? v4[k].z : v4[k].w;
+        if (nd == KC)
+          fold_chunk<KC, true>(v, nd, d0, m[p], S[p], T[p]);
+        else
+          fold_chunk<KC, false>(v, nd, d0, m[p], S[p], T[p]);
       }
     }
   }
@@ -256,7 +270,6 @@ __global__ __launch_bounds__(kThreads) void softargmin_f32x4_kernel(const float*
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       sm_m[wave - 1][p][lane] = m[p];
-      sm_p[wave - 1][p][lane] = probe[p];
       sm_s[wave - 1][p][lane] = S[p];
       sm_t[wave - 1][p][lane] = T[p];
     }
@@ -267,11 +280,7 @@ __global__ __launch_bounds__(kThreads) void softargmin_f32x4_kernel(const float*
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     float M = m[p];
-    float pr = probe[p];
-    for (int w = 0; w < 3; ++w) {
-      M = fmaxf(M, sm_m[w][p][lane]);
-      pr += sm_p[w][p][lane];
-    }
+    for (int w = 0; w < 3; ++w) M = fmaxf(M, sm_m[w][p][lane]);
     double Sa = 0.0, Ta = 0.0;
     if (M != -INFINITY && M != INFINITY) {
       if (m[p] != -INFINITY) {
@@ -287,8 +296,8 @@ __global__ __launch_bounds__(kThreads) void softargmin_f32x4_kernel(const float*
         Ta += sm_t[w][p][lane] * f;
       }
     }
-    // NaN anywhere in the column, an all -inf or any +inf column: NaN as in torch
-    res[p] = (D == 0) ? 0.f : (pr != pr || M == INFINITY || M == -INFINITY) ? NAN : (float)(Ta / Sa);
+    // an all -inf column, any +inf (or a poisoned pixel): NaN as in torch; NaN in S or T stays
+    res[p] = (D == 0) ? 0.f : (M == INFINITY || M == -INFINITY) ? NAN : (float)(Ta / Sa);
   }
   *reinterpret_cast<float4*>(out + (int64_t)n * W + x0) = make_float4(res[0], res[1], res[2], res[3]);
 }
@@ -411,9 +420,10 @@ int softargmin_entry(const void* volume, void* out, int dtype, int64_t N, int64_
     const int Wf = (int)W;
     const int64_t nunits = ceil_div(Wf, 64 * 4) * N;
     if (nunits > INT32_MAX) return fail(SM_EINVAL, "soft-argmin: too many pixels for one launch");
-    hipLaunchKernelGGL((softargmin_f32x4_kernel<8, true>), dim3((unsigned)nunits), dim3(kThreads),
-                       0, st, static_cast<const float*>(volume), static_cast<float*>(out), (int)D,
-                       Wf, vs.n, vs.d);
+    // 6 waves/SIMD (74 VGPRs); forcing 7 (72 VGPRs) or 8 (spills) measured no faster at r01
+    hipLaunchKernelGGL((softargmin_f32x4_kernel<8>), dim3((unsigned)nunits), dim3(kThreads), 0, st,
+                       static_cast<const float*>(volume), static_cast<float*>(out), (int)D, Wf,
+                       vs.n, vs.d);
     return check_launch("softargmin_f32x4_kernel");
   }
   const bool v4 = dtype == SM_F32 && (W % 4 == 0) && (vs.h % 4 == 0) && (vs.d % 4 == 0) &&
