@@ -271,6 +271,18 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
   const int wend = wbeg + q + (grp < rr ? 1 : 0);
   if (wbeg + gi >= wend) return;  // the whole workgroup leaves together
   const int nitems = (wend - (wbeg + gi) + gsz - 1) / gsz;
+  // item i of this workgroup is group-local index j = gi + i gsz.  With gsz % 8 == 0 every
+  // workgroup would keep one tile index (j % 8) for the whole launch, so the workgroups of the
+  // 64-pixel last tile of a 960-pixel row would idle half the time; rotating each complete
+  // aligned 8-item block by the round i = j / gsz spreads the short tiles over all workgroups.
+  // The set of items in flight per round (and so the L2 sharing) is unchanged.
+  const int wcnt = wend - wbeg;
+  const bool rot = (gsz & 7) == 0;
+  auto witem = [&](int i) -> int {
+    const int j = gi + i * gsz;
+    const int b = j & ~7;
+    return wbeg + ((rot && b + 8 <= wcnt) ? (b | ((j + i) & 7)) : j);
+  };
   const int nks = (cpg + kKC - 1) / kKC;
   const bool store_vol = __builtin_amdgcn_readfirstlane(args.out != nullptr ? 1 : 0) != 0;
   // NGHWD quads are 16-B aligned only when D % 4 == 0
@@ -811,13 +823,13 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
     }
     ws = s;
     if (i >= nitems) return false;
-    w = decode(wbeg + gi + i * gsz, args, DMAX);
+    w = decode(witem(i), args, DMAX);
     return true;
   };
 
   // items it = 0 .. nitems-1 (work index wbeg + gi + it gsz), channel steps ks = 0 .. nks-1;
   // every load() is followed by exactly kPF touches (of the step after the loaded one)
-  Work cur = decode(wbeg + gi, args, DMAX);
+  Work cur = decode(witem(0), args, DMAX);
   {
     Work pk = cur;
     int pks = 0;
@@ -828,7 +840,7 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
   for (int it = 0, ks = 0; it < nitems;) {
     const bool last = ks == nks - 1;
     const bool more = !last || it + 1 < nitems;
-    const Work nx = last && more ? decode(wbeg + gi + (it + 1) * gsz, args, DMAX) : cur;
+    const Work nx = last && more ? decode(witem(it + 1), args, DMAX) : cur;
     Work pk = cur;
     int pks = 0;
     const bool pv = ahead(it, ks, 2, pk, pks);

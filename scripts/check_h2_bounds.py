@@ -46,7 +46,15 @@ def work_lists(N, G, H, W, D, ncu):
         if wbeg + gi >= wend:
             continue
         nitems = (wend - (wbeg + gi) + gsz - 1) // gsz
-        yield blk, [wbeg + gi + it * gsz for it in range(nitems)]
+        yield blk, [witem(wbeg, wend, gi, gsz, it) for it in range(nitems)]
+
+
+def witem(wbeg, wend, gi, gsz, i):
+    """Mirror of band_h2's witem(): complete aligned 8-item blocks rotated by the round i."""
+    j = gi + i * gsz
+    b = j & ~7
+    rot = gsz % 8 == 0
+    return wbeg + ((b | ((j + i) & 7)) if rot and b + 8 <= wend - wbeg else j)
 
 
 def decode(w, tiles, npass, G, H, D, pw, DMAX):
