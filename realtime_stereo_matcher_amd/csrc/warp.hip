@@ -113,6 +113,16 @@ __global__ __launch_bounds__(kWarpThreads) void warp_rows_kernel(WarpArgs a, int
   const float dy = iy - fy0, sy = 1.0f - dy;
   const bool finite = fabsf(iy) < 2.0e9f;
   const int y0 = finite ? (int)fy0 : -2;
+  // the flow values of this lane's first kPre pixels are loaded before the staging loads, so
+  // their latency overlaps the rows' instead of following the barrier
+  const float* fl = a.flow + n * a.fsn + (int64_t)y * a.fsh;
+  constexpr int kPre = 4;
+  float fv[kPre];
+#pragma unroll
+  for (int k = 0; k < kPre; ++k) {
+    const int x = threadIdx.x + k * kWarpThreads;
+    fv[k] = x < a.W ? fl[x] : 0.f;
+  }
   // ---- stage rows y0, y0 + 1 of channels c0 .. c0 + nc (all loads of a lane issued first)
   const float* ib = a.img + n * a.isn + (int64_t)c0 * a.isc;
   const bool r0ok = y0 >= 0 && y0 < a.Hi, r1ok = y0 + 1 >= 0 && y0 + 1 < a.Hi;
@@ -146,26 +156,43 @@ __global__ __launch_bounds__(kWarpThreads) void warp_rows_kernel(WarpArgs a, int
       srow[r * RS + 4 + q] = ok ? ib[(int64_t)(r >> 1) * a.isc + ((r & 1) ? roff1 : roff0) + q] : 0.f;
     }
   }
-  __syncthreads();
   const int64_t HW = (int64_t)a.H * a.W;
   float* ob = a.out + ((int64_t)n * a.C + c0) * HW + (int64_t)y * a.W;
-  const float* fl = a.flow + n * a.fsn + (int64_t)y * a.fsh;
-  for (int x = threadIdx.x; x < a.W; x += kWarpThreads) {
-    float gx = (float)x - fl[x];
+  // pixel x with flow f: LDS columns of its two corners and the four bilinear weights
+  auto corners = [&](int x, float f, int& ia, int& ib2, float (&w)[4]) {
+    float gx = (float)x - f;
     gx = 2.0f * gx / a.dw - 1.0f;
     const float ix = (gx + 1.0f) * a.sx - 0.5f;
     const float fx0 = floorf(ix);
     const float dx = ix - fx0, ex = 1.0f - dx;
-    const float w0 = sy * ex, w1 = sy * dx, w2 = dy * ex, w3 = dy * dx;  // nw, ne, sw, se
+    w[0] = sy * ex, w[1] = sy * dx, w[2] = dy * ex, w[3] = dy * dx;  // nw, ne, sw, se
     const bool ok = finite && fabsf(ix) < 2.0e9f;
     const int x0 = ok ? (int)fx0 : -2;
-    const int ia = (ok && x0 >= 0 && x0 < a.Wi) ? x0 + 4 : 3;
-    const int ib2 = (ok && x0 + 1 >= 0 && x0 + 1 < a.Wi) ? x0 + 5 : 3;
+    ia = (ok && x0 >= 0 && x0 < a.Wi) ? x0 + 4 : 3;
+    ib2 = (ok && x0 + 1 >= 0 && x0 + 1 < a.Wi) ? x0 + 5 : 3;
+  };
+  auto blend = [&](int x, int ia, int ib2, const float (&w)[4]) {
     for (int c = 0; c < nc; ++c) {
       const float* s0 = srow + (2 * c) * RS;
       const float* s1 = s0 + RS;
-      ob[(int64_t)c * HW + x] = s0[ia] * w0 + s0[ib2] * w1 + s1[ia] * w2 + s1[ib2] * w3;
+      ob[(int64_t)c * HW + x] = s0[ia] * w[0] + s0[ib2] * w[1] + s1[ia] * w[2] + s1[ib2] * w[3];
     }
+  };
+  int pa[kPre], pb[kPre];
+  float pw[kPre][4];
+#pragma unroll
+  for (int k = 0; k < kPre; ++k) corners(threadIdx.x + k * kWarpThreads, fv[k], pa[k], pb[k], pw[k]);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kPre; ++k) {
+    const int x = threadIdx.x + k * kWarpThreads;
+    if (x < a.W) blend(x, pa[k], pb[k], pw[k]);
+  }
+  for (int x = threadIdx.x + kPre * kWarpThreads; x < a.W; x += kWarpThreads) {  // W > 1024
+    int ia, ib2;
+    float w[4];
+    corners(x, fl[x], ia, ib2, w);
+    blend(x, ia, ib2, w);
   }
 }
 

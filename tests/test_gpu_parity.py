@@ -623,7 +623,8 @@ def test_golden_warp(rec):
 
 
 @pytest.mark.parametrize("ish,fsh", [((2, 7, 33, 65), (2, 1, 33, 65)), ((1, 3, 17, 30), (1, 2, 40, 61)),
-                                     ((1, 5, 1, 9), (1, 1, 2, 9)), ((3, 1, 8, 8), (3, 2, 8, 8))])
+                                     ((1, 5, 1, 9), (1, 1, 2, 9)), ((3, 1, 8, 8), (3, 2, 8, 8)),
+                                     ((1, 9, 6, 1100), (1, 1, 6, 1100)), ((1, 2, 3, 5000), (1, 1, 3, 5000))])
 def test_warp_vs_oracle(ish, fsh):
     from realtime_stereo_matcher_amd.functional import warp_by_flow_map
 
