@@ -367,6 +367,94 @@ __global__ __launch_bounds__(kThreads) void argext_kernel(const T* __restrict__ 
   out[((int64_t)n * H + y) * W + x] = I < 0 ? 0 : I;
 }
 
+// fp32 argext over a flat contiguous plane, 4 pixels per lane (float4 loads of KC planes in
+// flight), same 4-wave D split and the same first-index / NaN-wins rules as argext_kernel.
+template <bool MAXMODE, int KC>
+__global__ __launch_bounds__(kThreads) void argext_f32x4_kernel(const float* __restrict__ vol,
+                                                                int64_t* __restrict__ out, int D,
+                                                                int W, int64_t vsn, int64_t vsd) {
+  __shared__ float sm_b[3][4][64];
+  __shared__ int sm_i[3][4][64];
+  const int P = (W + 255) >> 8;
+  const int unit = blockIdx.x;
+  const int n = unit / P;
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int x0 = ((unit - n * P) * 64 + lane) * 4;
+  const bool any = x0 < W;
+  const int Dq = (D + 3) >> 2;
+  const int dbeg = min(D, wave * Dq);
+  const int dend = min(D, dbeg + Dq);
+  const float* base = vol + n * vsn + (any ? x0 : 0);
+  float best[4];
+  int idx[4];
+  bool nanb[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    best[p] = MAXMODE ? -INFINITY : INFINITY;
+    idx[p] = -1;  // -1: this quarter is empty
+    nanb[p] = false;
+  }
+  if (any) {
+    for (int d0 = dbeg; d0 < dend; d0 += KC) {
+      float4 v4[KC];
+#pragma unroll
+      for (int k = 0; k < KC; ++k)
+        v4[k] = *reinterpret_cast<const float4*>(base + (int64_t)min(d0 + k, dend - 1) * vsd);
+#pragma unroll
+      for (int k = 0; k < KC; ++k) {
+        if (d0 + k < dend) {
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            const float v = p == 0 ? v4[k].x : p == 1 ? v4[k].y : p == 2 ? v4[k].z : v4[k].w;
+            const bool vnan = v != v;
+            const bool better = idx[p] < 0 || (MAXMODE ? (v > best[p]) : (v < best[p]));
+            if (!nanb[p] && (vnan || better)) {
+              best[p] = v;
+              idx[p] = d0 + k;
+              nanb[p] = vnan;
+            }
+          }
+        }
+      }
+    }
+  }
+  if (wave != 0) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      sm_b[wave - 1][p][lane] = best[p];
+      sm_i[wave - 1][p][lane] = idx[p];
+    }
+  }
+  __syncthreads();
+  if (wave != 0 || !any) return;
+  long long r[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    float B = best[p];
+    int I = idx[p];
+    for (int w = 0; w < 3; ++w) {  // quarters in disparity order
+      const int iw = sm_i[w][p][lane];
+      if (iw < 0) continue;
+      const float bw = sm_b[w][p][lane];
+      if (I < 0) {
+        B = bw;
+        I = iw;
+        continue;
+      }
+      if (B != B) break;  // a NaN already won
+      if ((bw != bw) || (MAXMODE ? (bw > B) : (bw < B))) {
+        B = bw;
+        I = iw;
+      }
+    }
+    r[p] = I < 0 ? 0 : I;
+  }
+  int64_t* o = out + (int64_t)n * W + x0;
+  reinterpret_cast<longlong2*>(o)[0] = make_longlong2(r[0], r[1]);
+  reinterpret_cast<longlong2*>(o)[1] = make_longlong2(r[2], r[3]);
+}
+
 int check_vol(const void* volume, const void* out, int dtype, int64_t N, int64_t D, int64_t H,
               int64_t W, const int64_t* s, VolView* vs) {
   if (!valid_dtype(dtype)) return fail(SM_EDTYPE, "unsupported dtype code");
@@ -462,6 +550,20 @@ int argext_entry(const void* volume, int64_t* out, int dtype, int64_t N, int64_t
   if (D <= 0) return fail(SM_EINVAL, "argext over an empty D axis");
   hipStream_t st = as_stream(stream);
   flatten_plane(vs, &H, &W);
+  if (dtype == SM_F32 && H == 1 && W % 4 == 0 && vs.d % 4 == 0 && vs.n % 4 == 0 &&
+      W < ((int64_t)1 << 30) && ((reinterpret_cast<uintptr_t>(volume) & 15u) == 0) &&
+      ((reinterpret_cast<uintptr_t>(out) & 15u) == 0)) {
+    const int64_t nunits = ceil_div(W, 64 * 4) * N;
+    if (nunits > INT32_MAX) return fail(SM_EINVAL, "argext: too many pixels for one launch");
+    const float* v = static_cast<const float*>(volume);
+    if (mode == SM_ARGMAX)
+      hipLaunchKernelGGL((argext_f32x4_kernel<true, 8>), dim3((unsigned)nunits), dim3(kThreads), 0,
+                         st, v, out, (int)D, (int)W, vs.n, vs.d);
+    else
+      hipLaunchKernelGGL((argext_f32x4_kernel<false, 8>), dim3((unsigned)nunits), dim3(kThreads), 0,
+                         st, v, out, (int)D, (int)W, vs.n, vs.d);
+    return check_launch("argext_f32x4_kernel");
+  }
   dim3 grid((unsigned)ceil_div(W, 64), (unsigned)H, (unsigned)N);
   SM_DISPATCH_DTYPE(dtype, T, {
     const T* v = static_cast<const T*>(volume);

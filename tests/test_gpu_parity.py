@@ -396,6 +396,12 @@ def test_regression_special_values_flat(W):
     got = host(F.soft_argmin(dev(v), keepdim=False))
     np.testing.assert_allclose(got, ref, atol=2e-5, equal_nan=True)
     np.testing.assert_array_equal(np.isnan(got), np.isnan(ref))
+    # hard argext on the same columns (flat fp32 kernel for W = 8): NaN wins, first index on ties
+    vt = v.copy()
+    vt[1, :, 0, 0] = 3.0                         # all tied -> 0
+    vt[1, 10:, 0, 1] = 5.0                       # tie from d = 10 on
+    np.testing.assert_array_equal(host(F.hard_argmax(dev(vt))), torch.argmax(torch.from_numpy(vt), 1).numpy())
+    np.testing.assert_array_equal(host(F.hard_argmin(dev(vt))), torch.argmin(torch.from_numpy(vt), 1).numpy())
 
 
 def test_zero_channels_and_empty():
