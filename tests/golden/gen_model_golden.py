@@ -1,0 +1,53 @@
+"""Model-level golden vectors for the §8f-3 drop-in demo (CONTAINER-ONLY).
+
+Imports the reference network ``MobileStereoNet`` (model/mobile_stereo_net.py:89-158) from
+``/root/reference`` at run time (``python3 -B``), builds it with a seeded random init (no
+checkpoint ships with the reference), randomises the BatchNorm statistics so eval mode is not an
+identity, and records in ``model_msn_v1.npz``: the state_dict (``sd/<key>``), a left/right image
+pair of 1x3x60x90 (not a multiple of 8: exercises the reference padding) and the reference's
+three eval-mode outputs on CPU.  Only data is written.
+
+Usage:  cd /root/repo && python3 -B tests/golden/gen_model_golden.py
+"""
+import importlib.util
+import os
+import sys
+
+import numpy as np
+import torch
+
+REF = "/root/reference"
+OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "model_msn_v1.npz")
+sys.dont_write_bytecode = True
+
+
+def main():
+    spec = importlib.util.spec_from_file_location("ref_msn", os.path.join(REF, "model/mobile_stereo_net.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    torch.manual_seed(0)
+    net = mod.MobileStereoNet()
+    g = torch.Generator().manual_seed(1)
+    with torch.no_grad():
+        for m in net.modules():
+            if isinstance(m, (torch.nn.BatchNorm2d, torch.nn.BatchNorm3d)):
+                m.running_mean.copy_(torch.randn(m.running_mean.shape, generator=g) * 0.1)
+                m.running_var.copy_(torch.rand(m.running_var.shape, generator=g) * 0.5 + 0.75)
+                m.weight.copy_(torch.rand(m.weight.shape, generator=g) * 0.5 + 0.75)
+                m.bias.copy_(torch.randn(m.bias.shape, generator=g) * 0.1)
+    net.eval()
+    rng = np.random.default_rng(7)
+    left = rng.uniform(0, 255, (1, 3, 60, 90)).astype(np.float32)
+    right = np.roll(left, -5, axis=3) + rng.normal(0, 2, left.shape).astype(np.float32)  # ~5 px shift
+    with torch.no_grad():
+        outs = net(torch.from_numpy(left), torch.from_numpy(right))
+    arrays = {f"sd/{k}": v.detach().numpy() for k, v in net.state_dict().items()}
+    arrays.update(left=left, right=right.astype(np.float32))
+    for i, o in enumerate(outs):
+        arrays[f"out{i}"] = o.numpy()
+    np.savez_compressed(OUT, **arrays)
+    print(f"wrote {OUT}: {len(arrays)} arrays, outputs {[tuple(o.shape) for o in outs]}")
+
+
+if __name__ == "__main__":
+    main()
