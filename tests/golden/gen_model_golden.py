@@ -1,9 +1,11 @@
 """Model-level golden vectors for the §8f-3 drop-in demo (CONTAINER-ONLY).
 
-Imports the reference network ``MobileStereoNet`` (model/mobile_stereo_net.py:89-158) from
+Imports the reference networks ``MobileStereoNet`` (model/mobile_stereo_net.py:89-158) and
+``MobileStereoNetV2`` (model/mobile_stereo_net_v2.py:136-232, the parameters of
+configure/stereo_net_config_v2.json) from
 ``/root/reference`` at run time (``python3 -B``), builds it with a seeded random init (no
 checkpoint ships with the reference), randomises the BatchNorm statistics so eval mode is not an
-identity, and records in ``model_msn_v1.npz``: the state_dict (``sd/<key>``), a left/right image
+identity, and records in ``model_msn_v1.npz`` / ``model_msn_v2.npz``: the state_dict (``sd/<key>``), a left/right image
 pair of 1x3x60x90 (not a multiple of 8: exercises the reference padding) and the reference's
 three eval-mode outputs on CPU.  Only data is written.
 
@@ -17,16 +19,21 @@ import numpy as np
 import torch
 
 REF = "/root/reference"
-OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "model_msn_v1.npz")
+OUT_DIR = os.path.dirname(os.path.abspath(__file__))
+V2_PARAMS = {"down_factor": 3, "max_disp": 192, "refine_dim": 7,
+             "refine_dilates": [1, 2, 4, 8, 1, 1], "hidden_dim": 32}  # stereo_net_config_v2.json
 sys.dont_write_bytecode = True
 
 
-def main():
-    spec = importlib.util.spec_from_file_location("ref_msn", os.path.join(REF, "model/mobile_stereo_net.py"))
+def _load(path, name):
+    spec = importlib.util.spec_from_file_location(name, os.path.join(REF, path))
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
+    return mod
+
+
+def record(net, out_name):
     torch.manual_seed(0)
-    net = mod.MobileStereoNet()
     g = torch.Generator().manual_seed(1)
     with torch.no_grad():
         for m in net.modules():
@@ -45,8 +52,17 @@ def main():
     arrays.update(left=left, right=right.astype(np.float32))
     for i, o in enumerate(outs):
         arrays[f"out{i}"] = o.numpy()
-    np.savez_compressed(OUT, **arrays)
-    print(f"wrote {OUT}: {len(arrays)} arrays, outputs {[tuple(o.shape) for o in outs]}")
+    out = os.path.join(OUT_DIR, out_name)
+    np.savez_compressed(out, **arrays)
+    print(f"wrote {out}: {len(arrays)} arrays, outputs {[tuple(o.shape) for o in outs]}")
+
+
+def main():
+    torch.manual_seed(0)
+    record(_load("model/mobile_stereo_net.py", "ref_msn").MobileStereoNet(), "model_msn_v1.npz")
+    torch.manual_seed(0)
+    record(_load("model/mobile_stereo_net_v2.py", "ref_msn_v2").MobileStereoNetV2(**V2_PARAMS),
+           "model_msn_v2.npz")
 
 
 if __name__ == "__main__":

@@ -1,41 +1,47 @@
-"""§8f-3 model-level drop-in demo: MobileStereoNet (v1) with the HIP cost volume and soft-argmin
-(realtime_stereo_matcher_amd/model/stereo_net_v1.py) against the reference network's own eval
-outputs, recorded from a seeded-init reference model (tests/golden/gen_model_golden.py)."""
+"""§8f-3 model-level drop-in demo: MobileStereoNet v1 / v2 with the HIP cost volume, soft-argmin
+and (v2) refinement warp (realtime_stereo_matcher_amd/model/stereo_nets.py) against the reference
+networks' own eval outputs, recorded from seeded-init reference models
+(tests/golden/gen_model_golden.py)."""
 import os
 
 import numpy as np
 import pytest
 import torch
 
-FIX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "model_msn_v1.npz")
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+# constructor arguments of the reference configs (stereo_net_config.json, stereo_net_config_v2.json)
+NETS = {"v1": {}, "v2": {"levels": 3, "max_disp": 192, "hidden_dim": 32, "v2": True, "refine_dim": 7,
+                        "refine_dilates": (1, 2, 4, 8, 1, 1)}}
 
 
-def _fixture():
-    return np.load(FIX)  # allow_pickle=False (default): data only
+def _fixture(v):
+    return np.load(os.path.join(GOLDEN, f"model_msn_{v}.npz"))  # allow_pickle=False: data only
 
 
-def _net(a):
-    from realtime_stereo_matcher_amd.model.stereo_net_v1 import MobileStereoNetHIP
+def _net(a, v):
+    from realtime_stereo_matcher_amd.model.stereo_nets import MobileStereoNetHIP
 
-    net = MobileStereoNetHIP()
+    net = MobileStereoNetHIP(**NETS[v])
     sd = {k[3:]: torch.from_numpy(a[k]) for k in a.files if k.startswith("sd/")}
     net.load_state_dict(sd, strict=True)
     return net.eval()
 
 
-def test_state_dict_matches_reference_layout():
+@pytest.mark.parametrize("v", sorted(NETS))
+def test_state_dict_matches_reference_layout(v):
     """CPU: the demo network takes the reference network's state_dict unchanged."""
-    _net(_fixture())
+    _net(_fixture(v), v)
 
 
 @pytest.mark.gpu
-def test_model_outputs_match_reference():
+@pytest.mark.parametrize("v", sorted(NETS))
+def test_model_outputs_match_reference(v):
     """GPU: all three refinement outputs within 2e-3 px of the reference's (|disp| ~ 65..105 px
     at full resolution; the difference is MIOpen-vs-CPU convolution rounding through 3 stages)."""
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
-    a = _fixture()
-    net = _net(a).cuda()
+    a = _fixture(v)
+    net = _net(a, v).cuda()
     with torch.no_grad():
         outs = net(torch.from_numpy(a["left"]).cuda(), torch.from_numpy(a["right"]).cuda())
     assert len(outs) == 3
