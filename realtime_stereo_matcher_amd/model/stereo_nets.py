@@ -107,3 +107,122 @@ class MobileStereoNetHIP(nn.Module):
             full = F.interpolate(disp * scale, tuple(left.shape[2:]))[:, :, :h, :w]
             outs.append(-full)
         return outs
+
+
+# ------------------------------------------------------------------------------------ v3
+class _SamePadConv(nn.Conv2d):
+    """Strided conv with TensorFlow-style 'same' padding, extra pixel bottom/right (reference
+    same_padding_conv / SameConv2d, model/mobile_stereo_net_v3.py:145-167)."""
+
+    def forward(self, x):
+        (kh, kw), (sh, sw) = self.kernel_size, self.stride
+        ph = max((-(-x.shape[2] // sh) - 1) * sh + kh - x.shape[2], 0)
+        pw = max((-(-x.shape[3] // sw) - 1) * sw + kw - x.shape[3], 0)
+        x = F.pad(x, (pw // 2, pw - pw // 2, ph // 2, ph - ph // 2))
+        return F.conv2d(x, self.weight, self.bias, stride=self.stride)
+
+
+def _lrelu():
+    return nn.LeakyReLU(0.2)
+
+
+class _Up(nn.Module):
+    """2x transposed-conv upsample merged with the skip connection (reference UpsampleBlock,
+    v3 :170-190)."""
+
+    def __init__(self, cin, cout):
+        super().__init__()
+        self.up_conv = nn.Sequential(nn.ConvTranspose2d(cin, cout, 2, 2), _lrelu())
+        self.merge_conv = nn.Sequential(nn.Conv2d(2 * cout, cout, 1), _lrelu(),
+                                        nn.Conv2d(cout, cout, 3, 1, 1), _lrelu(),
+                                        nn.Conv2d(cout, cout, 3, 1, 1), _lrelu())
+
+    def forward(self, x, skip):
+        return self.merge_conv(torch.cat((self.up_conv(x), skip), dim=1))
+
+
+class _UNet(nn.Module):
+    """Feature pyramid, coarsest first (reference UNetFeatureExtractor, v3 :193-246)."""
+
+    def __init__(self, dims):
+        super().__init__()
+        levels = len(dims) - 1
+        self.down_layers = nn.ModuleList()
+        for i in range(levels + 1):
+            if i == 0:
+                mods = [nn.Conv2d(3, dims[0], 3, 1, 1), _lrelu()]
+            else:
+                mods = [_SamePadConv(dims[i - 1], dims[i], 4, 2), _lrelu()]
+                for _ in range(3 if i == levels else 1):
+                    mods += [nn.Conv2d(dims[i], dims[i], 3, 1, 1), _lrelu()]
+            self.down_layers.append(nn.Sequential(*mods))
+        self.up_layers = nn.ModuleList(_Up(dims[j], dims[j - 1]) for j in range(levels, 0, -1))
+
+    def forward(self, x):
+        skips = []
+        for layer in self.down_layers:
+            x = layer(x)
+            skips.append(x)
+        pyramid = [x]
+        for i, up in enumerate(self.up_layers):
+            x = up(x, skips[len(skips) - 2 - i])
+            pyramid.append(x)
+        return pyramid
+
+
+class _RefineFeat(nn.Module):
+    """v3 refinement: the upsampled disparity, the left feature map and the right feature map
+    warped by that disparity (reference RefineNet, v3 :100-140)."""
+
+    def __init__(self, in_dim, hidden, dilations):
+        super().__init__()
+        layers = [_cbr(in_dim, hidden)] + [_Residual(hidden, d) for d in dilations]
+        layers.append(nn.Conv2d(hidden, 1, 3, 1, 1))
+        self.conv0 = nn.Sequential(*layers)
+
+    def forward(self, disp, l_fmap, r_fmap):
+        up = 2 * F.interpolate(disp, scale_factor=2, mode="bilinear", align_corners=False)
+        size = tuple(up.shape[2:])
+        if tuple(l_fmap.shape[2:]) != size or tuple(r_fmap.shape[2:]) != size:
+            l_fmap = F.interpolate(l_fmap, size, mode="bilinear", align_corners=False)
+            r_fmap = F.interpolate(r_fmap, size, mode="bilinear", align_corners=False)
+        r_fmap = warp_by_flow_map(r_fmap, up)                          # HIP: sm_warp_by_flow
+        residual = self.conv0(torch.cat((up, l_fmap, r_fmap), dim=1))
+        return F.relu(up + residual)
+
+
+class MobileStereoNetV3HIP(nn.Module):
+    """MobileStereoNetV3 (reference v3 :249-336, configure/stereo_net_config_v3.json) with the HIP
+    difference volume, soft-argmin and feature-map warp."""
+
+    def __init__(self, down_factor=3, max_disp=192, refine_dilates=(1, 2, 4, 8, 1, 1), hidden_dim=32):
+        super().__init__()
+        self.down_factor = down_factor
+        self.align = 1 << down_factor
+        self.max_disp = (max_disp + 1) >> down_factor
+        self.feature_extractor = _UNet([hidden_dim] * (down_factor + 1))
+        hd = hidden_dim
+        filt = []
+        for _ in range(4):
+            filt += [nn.Conv3d(hd, hd, 3, 1, 1), nn.BatchNorm3d(hd), nn.ReLU()]
+        filt.append(nn.Conv3d(hd, 1, 3, 1, 1))
+        self.cost_filter = nn.Sequential(*filt)
+        self.refine_layers = nn.ModuleList(
+            _RefineFeat(1 + 2 * hd, hd, tuple(refine_dilates)) for _ in range(down_factor))
+
+    def forward(self, l_img, r_img):
+        norm = lambda im: (2.0 * (im / 255.0) - 1.0).contiguous()  # noqa: E731
+        left, right = norm(l_img), norm(r_img)
+        h, w = left.shape[2:]
+        pad = (0, (-w) % self.align, 0, (-h) % self.align)
+        left, right = F.pad(left, pad), F.pad(right, pad)
+        lp = self.feature_extractor(left)
+        rp = self.feature_extractor(right)
+        volume = make_cost_volume(lp[0], rp[0], self.max_disp)          # HIP: sm_cv_diff
+        disp = soft_argmin_regression(self.cost_filter(volume).squeeze(1))  # HIP: soft-argmin
+        outs = []
+        for i, refine in enumerate(self.refine_layers):
+            disp = refine(disp, lp[i + 1], rp[i + 1])
+            scale = left.shape[3] / disp.shape[3]
+            outs.append(-F.interpolate(disp * scale, tuple(left.shape[2:]))[:, :, :h, :w])
+        return outs

@@ -1,11 +1,11 @@
 """Model-level golden vectors for the §8f-3 drop-in demo (CONTAINER-ONLY).
 
 Imports the reference networks ``MobileStereoNet`` (model/mobile_stereo_net.py:89-158) and
-``MobileStereoNetV2`` (model/mobile_stereo_net_v2.py:136-232, the parameters of
-configure/stereo_net_config_v2.json) from
+``MobileStereoNetV2`` (model/mobile_stereo_net_v2.py:136-232) and ``MobileStereoNetV3``
+(model/mobile_stereo_net_v3.py:249-336), with the parameters of their configure/*.json, from
 ``/root/reference`` at run time (``python3 -B``), builds it with a seeded random init (no
 checkpoint ships with the reference), randomises the BatchNorm statistics so eval mode is not an
-identity, and records in ``model_msn_v1.npz`` / ``model_msn_v2.npz``: the state_dict (``sd/<key>``), a left/right image
+identity, and records in ``model_msn_v{1,2,3}.npz``: the state_dict (``sd/<key>``), a left/right image
 pair of 1x3x60x90 (not a multiple of 8: exercises the reference padding) and the reference's
 three eval-mode outputs on CPU.  Only data is written.
 
@@ -22,6 +22,8 @@ REF = "/root/reference"
 OUT_DIR = os.path.dirname(os.path.abspath(__file__))
 V2_PARAMS = {"down_factor": 3, "max_disp": 192, "refine_dim": 7,
              "refine_dilates": [1, 2, 4, 8, 1, 1], "hidden_dim": 32}  # stereo_net_config_v2.json
+V3_PARAMS = {"down_factor": 3, "max_disp": 192, "refine_dilates": [1, 2, 4, 8, 1, 1],
+             "hidden_dim": 32}  # stereo_net_config_v3.json
 sys.dont_write_bytecode = True
 
 
@@ -63,6 +65,9 @@ def main():
     torch.manual_seed(0)
     record(_load("model/mobile_stereo_net_v2.py", "ref_msn_v2").MobileStereoNetV2(**V2_PARAMS),
            "model_msn_v2.npz")
+    torch.manual_seed(0)
+    record(_load("model/mobile_stereo_net_v3.py", "ref_msn_v3").MobileStereoNetV3(**V3_PARAMS),
+           "model_msn_v3.npz")
 
 
 if __name__ == "__main__":

@@ -1,5 +1,5 @@
-"""§8f-3 model-level drop-in demo: MobileStereoNet v1 / v2 with the HIP cost volume, soft-argmin
-and (v2) refinement warp (realtime_stereo_matcher_amd/model/stereo_nets.py) against the reference
+"""§8f-3 model-level drop-in demo: MobileStereoNet v1 / v2 / v3 with the HIP cost volume,
+soft-argmin and (v2, v3) refinement warp (realtime_stereo_matcher_amd/model/stereo_nets.py) against the reference
 networks' own eval outputs, recorded from seeded-init reference models
 (tests/golden/gen_model_golden.py)."""
 import os
@@ -10,8 +10,11 @@ import torch
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 # constructor arguments of the reference configs (stereo_net_config.json, stereo_net_config_v2.json)
-NETS = {"v1": {}, "v2": {"levels": 3, "max_disp": 192, "hidden_dim": 32, "v2": True, "refine_dim": 7,
-                        "refine_dilates": (1, 2, 4, 8, 1, 1)}}
+NETS = {"v1": ("MobileStereoNetHIP", {}),
+        "v2": ("MobileStereoNetHIP", {"levels": 3, "max_disp": 192, "hidden_dim": 32, "v2": True,
+                                      "refine_dim": 7, "refine_dilates": (1, 2, 4, 8, 1, 1)}),
+        "v3": ("MobileStereoNetV3HIP", {"down_factor": 3, "max_disp": 192,
+                                        "refine_dilates": (1, 2, 4, 8, 1, 1), "hidden_dim": 32})}
 
 
 def _fixture(v):
@@ -19,9 +22,10 @@ def _fixture(v):
 
 
 def _net(a, v):
-    from realtime_stereo_matcher_amd.model.stereo_nets import MobileStereoNetHIP
+    from realtime_stereo_matcher_amd.model import stereo_nets
 
-    net = MobileStereoNetHIP(**NETS[v])
+    cls, kw = NETS[v]
+    net = getattr(stereo_nets, cls)(**kw)
     sd = {k[3:]: torch.from_numpy(a[k]) for k in a.files if k.startswith("sd/")}
     net.load_state_dict(sd, strict=True)
     return net.eval()
