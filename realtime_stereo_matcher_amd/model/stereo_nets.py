@@ -226,3 +226,131 @@ class MobileStereoNetV3HIP(nn.Module):
             scale = left.shape[3] / disp.shape[3]
             outs.append(-F.interpolate(disp * scale, tuple(left.shape[2:]))[:, :, :h, :w])
         return outs
+
+
+# ------------------------------------------------------------------------------ DispNetC
+class _Layer(nn.Module):
+    """Holds one Sequential under the attribute name ``layer`` (the reference blocks' layout)."""
+
+    def __init__(self, *mods):
+        super().__init__()
+        self.layer = nn.Sequential(*mods)
+
+    def forward(self, x):
+        return self.layer(x)
+
+
+def _conv_block(cin, cout, k, stride=1, bn=True):
+    """k x k conv (no bias, 'same' padding for odd k) [-> BN] -> LeakyReLU(0.1)
+    (reference Conv2dBlock, model/mobile_disp_net_c.py:9-55)."""
+    mods = [nn.Conv2d(cin, cout, k, stride, (k - 1) // 2, bias=False)]
+    if bn:
+        mods.append(nn.BatchNorm2d(cout))
+    mods.append(nn.LeakyReLU(0.1))
+    return _Layer(*mods)
+
+
+def _deconv_block(cin, cout, k, stride, bn=True):
+    """Transposed conv doubling the size [-> BN] -> LeakyReLU(0.1) (reference
+    Conv2dTransposeBlock, :58-109)."""
+    mods = [nn.ConvTranspose2d(cin, cout, k, stride, (k - 1) // 2,
+                               output_padding=stride - 1 - int(k % 2 == 0), bias=False)]
+    if bn:
+        mods.append(nn.BatchNorm2d(cout))
+    mods.append(nn.LeakyReLU(0.1))
+    return _Layer(*mods)
+
+
+class _ResDown(nn.Module):
+    """Strided residual block with a projected shortcut (reference ResBlock, :112-141)."""
+
+    def __init__(self, cin, cout, stride=1):
+        super().__init__()
+        self.conv1 = nn.Conv2d(cin, cout, 3, stride, 1)
+        self.bn1 = nn.BatchNorm2d(cout)
+        self.relu = nn.ReLU()
+        self.conv2 = nn.Conv2d(cout, cout, 3, 1, 1)
+        self.bn2 = nn.BatchNorm2d(cout)
+        self.shortcut = (nn.Sequential(nn.Conv2d(cin, cout, 1, stride), nn.BatchNorm2d(cout))
+                         if stride != 1 or cin != cout else None)
+
+    def forward(self, x):
+        skip = x if self.shortcut is None else self.shortcut(x)
+        y = self.bn2(self.conv2(self.relu(self.bn1(self.conv1(x)))))
+        return self.relu(y + skip)
+
+
+class _UpPredict(nn.Module):
+    """Coarse disparity prediction plus 2x feature upsampling merged with the skip features
+    (reference UpsampleBlock, :144-185)."""
+
+    def __init__(self, cin, cskip, cout, bn=True):
+        super().__init__()
+        self.deconv = _deconv_block(cin, cout, 4, 2, bn)
+        self.predict = nn.Conv2d(cin, 1, 3, 1, 1, bias=False)
+        self.up_predict = nn.ConvTranspose2d(1, 1, 4, 2, 1, bias=False)
+        self.concat = nn.Conv2d(cskip + cout + 1, cout, 3, 1, 1, bias=False)
+
+    def forward(self, x, skip):
+        disp = self.predict(x)
+        merged = torch.cat((skip, self.deconv(x), self.up_predict(disp)), dim=1)
+        return disp, self.concat(merged)
+
+
+class MobileDispNetCHIP(nn.Module):
+    """MobileDispNetC (reference model/mobile_disp_net_c.py:237-412, configure/disp_net_c_config.json)
+    with the correlation volume (mean over channels, D = max_disp // 4) on the HIP band kernel
+    (sm_cv_correlation_mean)."""
+
+    def __init__(self, hidden_dim=32, max_disp=192, with_batch_norm=True):
+        super().__init__()
+        self.down_factor = 6
+        self.max_disp = max_disp
+        c, bn = hidden_dim, with_batch_norm
+        self.conv1 = _conv_block(3, c, 7, 2, bn)
+        self.conv2 = _conv_block(c, 2 * c, 5, 2, bn)
+        self.conv_redir = _conv_block(2 * c, c, 1, 1, bn)
+        self.conv3 = nn.Sequential(_conv_block(c + max_disp // 4, 4 * c, 5, 2, bn),
+                                   _conv_block(4 * c, 4 * c, 3, 1, False))
+        self.res4 = _ResDown(4 * c, 8 * c, 2)
+        self.res5 = _ResDown(8 * c, 16 * c, 2)
+        self.res6 = _ResDown(16 * c, 32 * c, 2)
+        self.up5 = _UpPredict(32 * c, 16 * c, 16 * c, bn)
+        self.up4 = _UpPredict(16 * c, 8 * c, 8 * c, bn)
+        self.up3 = _UpPredict(8 * c, 4 * c, 4 * c, bn)
+        self.up2 = _UpPredict(4 * c, 2 * c, 2 * c, bn)
+        self.up1 = _UpPredict(2 * c, c, c, bn)
+        self.predict = nn.Conv2d(c, 1, 3, 1, 1, bias=False)
+
+    @staticmethod
+    def _resize(disp, shape):
+        """reference disparity_interpolate (:223-234): bilinear resize with the x-scale applied."""
+        if tuple(disp.shape[2:]) != tuple(shape):
+            disp = F.interpolate(disp * (float(shape[1]) / disp.shape[3]), tuple(shape),
+                                 mode="bilinear", align_corners=False)
+        return disp
+
+    def forward(self, l_img, r_img):
+        from .mobile_disp_net_c import make_correlation_volume
+
+        norm = lambda im: (2.0 * (im / 255.0) - 1.0).contiguous()  # noqa: E731
+        left, right = norm(l_img), norm(r_img)
+        h, w = left.shape[2:]
+        align = 1 << self.down_factor
+        pad = (0, (-w) % align, 0, (-h) % align)
+        left, right = F.pad(left, pad), F.pad(right, pad)
+        l1, r1 = self.conv1(left), self.conv1(right)
+        l2, r2 = self.conv2(l1), self.conv2(r1)
+        corr = make_correlation_volume(l2, r2, self.max_disp // 4)     # HIP: sm_cv_correlation_mean
+        c3 = self.conv3(torch.cat((self.conv_redir(l2), corr), dim=1))
+        r4 = self.res4(c3)
+        r5 = self.res5(r4)
+        r6 = self.res6(r5)
+        d6, u = self.up5(r6, r5)
+        d5, u = self.up4(u, r4)
+        d4, u = self.up3(u, c3)
+        d3, u = self.up2(u, l2)
+        d2, u = self.up1(u, l1)
+        d1 = self.predict(u)
+        size = tuple(left.shape[2:])
+        return [-self._resize(d, size)[:, :, :h, :w] for d in (d6, d5, d4, d3, d2, d1)]

@@ -1,11 +1,12 @@
 """Model-level golden vectors for the §8f-3 drop-in demo (CONTAINER-ONLY).
 
 Imports the reference networks ``MobileStereoNet`` (model/mobile_stereo_net.py:89-158) and
-``MobileStereoNetV2`` (model/mobile_stereo_net_v2.py:136-232) and ``MobileStereoNetV3``
-(model/mobile_stereo_net_v3.py:249-336), with the parameters of their configure/*.json, from
+``MobileStereoNetV2`` (model/mobile_stereo_net_v2.py:136-232), ``MobileStereoNetV3``
+(model/mobile_stereo_net_v3.py:249-336) and ``MobileDispNetC`` (model/mobile_disp_net_c.py:237-412),
+with the parameters of their configure/*.json, from
 ``/root/reference`` at run time (``python3 -B``), builds it with a seeded random init (no
 checkpoint ships with the reference), randomises the BatchNorm statistics so eval mode is not an
-identity, and records in ``model_msn_v{1,2,3}.npz``: the state_dict (``sd/<key>``), a left/right image
+identity, and records in ``model_msn_v{1,2,3}.npz`` / ``model_dispnetc.npz``: the state_dict (``sd/<key>``), a left/right image
 pair of 1x3x60x90 (not a multiple of 8: exercises the reference padding) and the reference's
 three eval-mode outputs on CPU.  Only data is written.
 
@@ -22,6 +23,7 @@ REF = "/root/reference"
 OUT_DIR = os.path.dirname(os.path.abspath(__file__))
 V2_PARAMS = {"down_factor": 3, "max_disp": 192, "refine_dim": 7,
              "refine_dilates": [1, 2, 4, 8, 1, 1], "hidden_dim": 32}  # stereo_net_config_v2.json
+DNC_PARAMS = {"hidden_dim": 8, "max_disp": 192, "with_batch_norm": True}  # disp_net_c_config.json
 V3_PARAMS = {"down_factor": 3, "max_disp": 192, "refine_dilates": [1, 2, 4, 8, 1, 1],
              "hidden_dim": 32}  # stereo_net_config_v3.json
 sys.dont_write_bytecode = True
@@ -34,11 +36,18 @@ def _load(path, name):
     return mod
 
 
-def record(net, out_name):
+def record(net, out_name, hw=(60, 90), weight_seed=None):
+    """weight_seed: load synthetic weights from tests/model_weights.seeded_state instead of
+    storing the state_dict (keeps the larger networks' fixtures small)."""
     torch.manual_seed(0)
     g = torch.Generator().manual_seed(1)
+    if weight_seed is not None:
+        sys.path.insert(0, os.path.dirname(OUT_DIR))
+        from model_weights import seeded_state
+
+        net.load_state_dict(seeded_state(net.state_dict(), weight_seed))
     with torch.no_grad():
-        for m in net.modules():
+        for m in net.modules() if weight_seed is None else ():
             if isinstance(m, (torch.nn.BatchNorm2d, torch.nn.BatchNorm3d)):
                 m.running_mean.copy_(torch.randn(m.running_mean.shape, generator=g) * 0.1)
                 m.running_var.copy_(torch.rand(m.running_var.shape, generator=g) * 0.5 + 0.75)
@@ -46,11 +55,12 @@ def record(net, out_name):
                 m.bias.copy_(torch.randn(m.bias.shape, generator=g) * 0.1)
     net.eval()
     rng = np.random.default_rng(7)
-    left = rng.uniform(0, 255, (1, 3, 60, 90)).astype(np.float32)
+    left = rng.uniform(0, 255, (1, 3) + tuple(hw)).astype(np.float32)
     right = np.roll(left, -5, axis=3) + rng.normal(0, 2, left.shape).astype(np.float32)  # ~5 px shift
     with torch.no_grad():
         outs = net(torch.from_numpy(left), torch.from_numpy(right))
-    arrays = {f"sd/{k}": v.detach().numpy() for k, v in net.state_dict().items()}
+    arrays = ({f"sd/{k}": v.detach().numpy() for k, v in net.state_dict().items()}
+              if weight_seed is None else {"weight_seed": np.array(weight_seed)})
     arrays.update(left=left, right=right.astype(np.float32))
     for i, o in enumerate(outs):
         arrays[f"out{i}"] = o.numpy()
@@ -68,6 +78,10 @@ def main():
     torch.manual_seed(0)
     record(_load("model/mobile_stereo_net_v3.py", "ref_msn_v3").MobileStereoNetV3(**V3_PARAMS),
            "model_msn_v3.npz")
+    torch.manual_seed(0)
+    # 100 x 200 pads to 128 x 256: conv2 features 16 x 32 x 64, correlation D = 48 < W = 64
+    record(_load("model/mobile_disp_net_c.py", "ref_dnc").MobileDispNetC(**DNC_PARAMS),
+           "model_dispnetc.npz", hw=(100, 200), weight_seed=11)
 
 
 if __name__ == "__main__":

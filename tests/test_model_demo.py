@@ -1,5 +1,5 @@
-"""§8f-3 model-level drop-in demo: MobileStereoNet v1 / v2 / v3 with the HIP cost volume,
-soft-argmin and (v2, v3) refinement warp (realtime_stereo_matcher_amd/model/stereo_nets.py) against the reference
+"""§8f-3 model-level drop-in demo: MobileStereoNet v1 / v2 / v3 with the HIP difference volume,
+soft-argmin and (v2, v3) refinement warp, and MobileDispNetC with the HIP correlation volume (realtime_stereo_matcher_amd/model/stereo_nets.py) against the reference
 networks' own eval outputs, recorded from seeded-init reference models
 (tests/golden/gen_model_golden.py)."""
 import os
@@ -14,11 +14,14 @@ NETS = {"v1": ("MobileStereoNetHIP", {}),
         "v2": ("MobileStereoNetHIP", {"levels": 3, "max_disp": 192, "hidden_dim": 32, "v2": True,
                                       "refine_dim": 7, "refine_dilates": (1, 2, 4, 8, 1, 1)}),
         "v3": ("MobileStereoNetV3HIP", {"down_factor": 3, "max_disp": 192,
-                                        "refine_dilates": (1, 2, 4, 8, 1, 1), "hidden_dim": 32})}
+                                        "refine_dilates": (1, 2, 4, 8, 1, 1), "hidden_dim": 32}),
+        "dispnetc": ("MobileDispNetCHIP", {"hidden_dim": 8, "max_disp": 192, "with_batch_norm": True})}
+FILES = {"v1": "model_msn_v1.npz", "v2": "model_msn_v2.npz", "v3": "model_msn_v3.npz",
+         "dispnetc": "model_dispnetc.npz"}
 
 
 def _fixture(v):
-    return np.load(os.path.join(GOLDEN, f"model_msn_{v}.npz"))  # allow_pickle=False: data only
+    return np.load(os.path.join(GOLDEN, FILES[v]))  # allow_pickle=False: data only
 
 
 def _net(a, v):
@@ -26,7 +29,12 @@ def _net(a, v):
 
     cls, kw = NETS[v]
     net = getattr(stereo_nets, cls)(**kw)
-    sd = {k[3:]: torch.from_numpy(a[k]) for k in a.files if k.startswith("sd/")}
+    if "weight_seed" in a.files:  # synthetic weights regenerated from the recorded seed
+        from model_weights import seeded_state
+
+        sd = seeded_state(net.state_dict(), int(a["weight_seed"]))
+    else:
+        sd = {k[3:]: torch.from_numpy(a[k]) for k in a.files if k.startswith("sd/")}
     net.load_state_dict(sd, strict=True)
     return net.eval()
 
@@ -40,15 +48,16 @@ def test_state_dict_matches_reference_layout(v):
 @pytest.mark.gpu
 @pytest.mark.parametrize("v", sorted(NETS))
 def test_model_outputs_match_reference(v):
-    """GPU: all three refinement outputs within 2e-3 px of the reference's (|disp| ~ 65..105 px
-    at full resolution; the difference is MIOpen-vs-CPU convolution rounding through 3 stages)."""
+    """GPU: every output within 2e-3 px of the reference's (|disp| ~ 65..105 px for the
+    MobileStereoNets, O(1..10) for DispNetC's synthetic weights; the difference is MIOpen-vs-CPU
+    convolution rounding)."""
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     a = _fixture(v)
     net = _net(a, v).cuda()
     with torch.no_grad():
         outs = net(torch.from_numpy(a["left"]).cuda(), torch.from_numpy(a["right"]).cuda())
-    assert len(outs) == 3
+    assert len(outs) == (6 if v == "dispnetc" else 3)
     for i, o in enumerate(outs):
         ref = a[f"out{i}"]
         assert tuple(o.shape) == ref.shape
