@@ -234,6 +234,11 @@ def main():
         ("resize_n1c4h6w20_to_h12w40", (1, 4, 6, 20), (1, 1, 12, 40), lambda sh: rng.uniform(-5, 45, sh)),
         ("disp_n1c32h30w40", (1, 32, 30, 40), (1, 1, 30, 40), lambda sh: rng.uniform(0, 24, sh)),
         ("intdisp_n1c6h8w33", (1, 6, 8, 33), (1, 1, 8, 33), lambda sh: rng.integers(0, 12, sh)),
+        # degenerate grids: h = 1 / w = 1 divide by zero in the reference's normalisation -> NaN
+        ("degenerate_h1_n1c2h4w16", (1, 2, 4, 16), (1, 1, 1, 16), lambda sh: rng.uniform(0, 3, sh)),
+        ("degenerate_w1_n1c2h4w16", (1, 2, 4, 16), (1, 1, 4, 1), lambda sh: rng.uniform(0, 3, sh)),
+        ("nanflow_n1c3h6w20", (1, 3, 6, 20), (1, 2, 6, 20),
+         lambda sh: np.where(rng.uniform(size=sh) < 0.05, np.nan, rng.uniform(-4, 4, sh))),
     ]
     for name, ish, fsh, gen in warp_cases:
         img = torch.from_numpy(rng.standard_normal(ish).astype(np.float32))
