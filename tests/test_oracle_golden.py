@@ -163,3 +163,28 @@ def test_warp_assert_message(manifest):
     with pytest.raises(AssertionError) as e:
         O.warp_by_flow_map(np.zeros((1, 2, 3, 4), np.float32), np.zeros((1, 3, 3, 4), np.float32))
     assert str(e.value) == manifest["warp_assert_message_c3"]
+
+
+def test_warp_rows_subset_matches_full():
+    """The oracle's row-subset mode (used at full size on the GPU) equals the full evaluation."""
+    rng = np.random.default_rng(3)
+    img = rng.standard_normal((2, 3, 9, 21)).astype(np.float32)
+    for fch in (1, 2):
+        flow = rng.uniform(-3, 8, (2, fch, 9, 21)).astype(np.float32)
+        full = O.warp_by_flow_map(img, flow)
+        rows = [0, 4, 8]
+        np.testing.assert_array_equal(O.warp_by_flow_map(img, flow, rows=rows), full[:, :, rows])
+
+
+def test_model_weights_deterministic():
+    """tests/model_weights.seeded_state is a pure function of (layout, seed)."""
+    from model_weights import seeded_state
+
+    layout = {"a.weight": torch.zeros(4, 3, 3, 3), "a.bias": torch.zeros(4),
+              "bn.weight": torch.zeros(4), "bn.bias": torch.zeros(4),
+              "bn.running_mean": torch.zeros(4), "bn.running_var": torch.zeros(4),
+              "bn.num_batches_tracked": torch.zeros((), dtype=torch.int64)}
+    s1, s2 = seeded_state(layout, 5), seeded_state(layout, 5)
+    assert all(torch.equal(s1[k], s2[k]) for k in layout)
+    assert not torch.equal(seeded_state(layout, 6)["a.weight"], s1["a.weight"])
+    assert float(s1["bn.running_var"].min()) >= 0.75
