@@ -11,7 +11,7 @@
 // with fp64 accumulators for sum(e) and sum(d*e): the result is within a few fp32 ulp of the
 // exact value, i.e. the parity error budget is torch's own fp32 noise.  A plane whose rows are
 // contiguous is addressed as one flat pixel axis (no block straddles a row end), and fp32
-// soft-argmin there takes softargmin_f32x4_kernel (fp32 per chunk, fp64 across chunks).
+// soft-argmin there takes softargmin_wave_kernel (fp32 per chunk, fp64 across chunks).
 #include "common.h"
 
 #include <math.h>
@@ -210,34 +210,26 @@ __device__ __forceinline__ void fold_chunk(const float (&v)[KC], int nd, int d0,
 }
 
 // fp32 soft-argmin over a volume whose (H, W) plane is contiguous, addressed as a flat pixel
-// axis (the host passes H = 1, W = H*W), so no block straddles a row end: cfg2's 518,400
-// pixels are exactly 2,025 blocks of 256.
-// Same 4-wave disparity split as softargmin_kernel.  Per KC-plane chunk each lane folds its 4
-// pixels in fp32 (sum e and sum k*e relative to the chunk start, k < KC, e = 2^((v-m) log2 e)
-// on v_exp_f32), and carries those into fp64 sums once per chunk: 0.6 fp64 ops per element
-// instead of 4, which is what kept the fp64-per-element kernel compute-bound.
-template <int KC>
-__global__ __launch_bounds__(kThreads) void softargmin_f32x4_kernel(const float* __restrict__ vol,
-                                                                    float* __restrict__ out,
-                                                                    int D, int W, int64_t vsn,
-                                                                    int64_t vsd) {
-  __shared__ float sm_m[3][4][64];
-  __shared__ double sm_s[3][4][64];
-  __shared__ double sm_t[3][4][64];
-  // unit = (n, 256-pixel group), n-major.  (Walking the units in the reverse of the order
-  // band_h2 writes them, so the freshest rows are read first, measured no faster at r01.)
+// axis (the host passes H = 1, W = H*W): one wave per unit = (n, 256-pixel group), 4 pixels per
+// lane, over ALL of D with KC float4 plane loads in flight.  Per chunk each lane folds its
+// pixels in fp32 (sum e and sum k*e relative to the chunk start, e = 2^((v-m) log2 e) on
+// v_exp_f32) and carries them into fp64 sums once per chunk: 0.6 fp64 ops per element instead
+// of 4.  No LDS merge and no barrier: a one-wave block retires as soon as its wave ends (r01,
+// cfg2: 74 us vs 79 us for 4 waves splitting D with an LDS merge, and vs 105 us for the first
+// fp64-per-element kernel).  WPB waves per block work on consecutive units.
+template <int KC, int WPB>
+__global__ __launch_bounds__(64 * WPB) void softargmin_wave_kernel(const float* __restrict__ vol,
+                                                                   float* __restrict__ out, int D,
+                                                                   int W, int64_t vsn, int64_t vsd,
+                                                                   int nunits) {
   const int P = (W + 255) >> 8;
-  const int unit = blockIdx.x;
+  const int unit = blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (unit >= nunits) return;
   const int n = unit / P;
-  const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const int x0 = ((unit - n * P) * 64 + lane) * 4;
-  const bool any = x0 < W;  // W % 4 == 0: a lane's 4 pixels are all in or all out
-  const int Dq = (D + 3) >> 2;
-  const int dbeg = min(D, wave * Dq);
-  const int dend = min(D, dbeg + Dq);
-  const float* base = vol + n * vsn + (any ? x0 : 0);
-
+  if (x0 >= W) return;
+  const float* base = vol + n * vsn + x0;
   float m[4];
   double S[4], T[4];
 #pragma unroll
@@ -246,59 +238,27 @@ __global__ __launch_bounds__(kThreads) void softargmin_f32x4_kernel(const float*
     S[p] = 0.0;
     T[p] = 0.0;
   }
-  if (any) {
-    for (int d0 = dbeg; d0 < dend; d0 += KC) {
-      const int nd = min(KC, dend - d0);
-      float4 v4[KC];
+  for (int d0 = 0; d0 < D; d0 += KC) {
+    const int nd = min(KC, D - d0);
+    float4 v4[KC];
 #pragma unroll
-      for (int k = 0; k < KC; ++k)
-        v4[k] = *reinterpret_cast<const float4*>(base + (int64_t)min(d0 + k, dend - 1) * vsd);
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        float v[KC];
-#pragma unroll
-        for (int k = 0; k < KC; ++k)
-          v[k] = p == 0 ? v4[k].x : p == 1 ? v4[k].y : p == 2 ? v4[k].z : v4[k].w;
-        if (nd == KC)
-          fold_chunk<KC, true>(v, nd, d0, m[p], S[p], T[p]);
-        else
-          fold_chunk<KC, false>(v, nd, d0, m[p], S[p], T[p]);
-      }
-    }
-  }
-  if (wave != 0) {
+    for (int k = 0; k < KC; ++k)
+      v4[k] = *reinterpret_cast<const float4*>(base + (int64_t)min(d0 + k, D - 1) * vsd);
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-      sm_m[wave - 1][p][lane] = m[p];
-      sm_s[wave - 1][p][lane] = S[p];
-      sm_t[wave - 1][p][lane] = T[p];
+      float v[KC];
+#pragma unroll
+      for (int k = 0; k < KC; ++k) v[k] = p == 0 ? v4[k].x : p == 1 ? v4[k].y : p == 2 ? v4[k].z : v4[k].w;
+      if (nd == KC)
+        fold_chunk<KC, true>(v, nd, d0, m[p], S[p], T[p]);
+      else
+        fold_chunk<KC, false>(v, nd, d0, m[p], S[p], T[p]);
     }
   }
-  __syncthreads();
-  if (wave != 0 || !any) return;
   float res[4];
 #pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    float M = m[p];
-    for (int w = 0; w < 3; ++w) M = fmaxf(M, sm_m[w][p][lane]);
-    double Sa = 0.0, Ta = 0.0;
-    if (M != -INFINITY && M != INFINITY) {
-      if (m[p] != -INFINITY) {
-        const double f = (double)expf(m[p] - M);
-        Sa = S[p] * f;
-        Ta = T[p] * f;
-      }
-      for (int w = 0; w < 3; ++w) {
-        const float mw = sm_m[w][p][lane];
-        if (mw == -INFINITY) continue;
-        const double f = (double)expf(mw - M);
-        Sa += sm_s[w][p][lane] * f;
-        Ta += sm_t[w][p][lane] * f;
-      }
-    }
-    // an all -inf column, any +inf (or a poisoned pixel): NaN as in torch; NaN in S or T stays
-    res[p] = (D == 0) ? 0.f : (M == INFINITY || M == -INFINITY) ? NAN : (float)(Ta / Sa);
-  }
+  for (int p = 0; p < 4; ++p)
+    res[p] = (D == 0) ? 0.f : (m[p] == INFINITY || m[p] == -INFINITY) ? NAN : (float)(T[p] / S[p]);
   *reinterpret_cast<float4*>(out + (int64_t)n * W + x0) = make_float4(res[0], res[1], res[2], res[3]);
 }
 
@@ -367,92 +327,55 @@ __global__ __launch_bounds__(kThreads) void argext_kernel(const T* __restrict__ 
   out[((int64_t)n * H + y) * W + x] = I < 0 ? 0 : I;
 }
 
-// fp32 argext over a flat contiguous plane, 4 pixels per lane (float4 loads of KC planes in
-// flight), same 4-wave D split and the same first-index / NaN-wins rules as argext_kernel.
+// fp32 argext over a flat contiguous plane: one wave per 256-pixel unit, 4 pixels per lane,
+// over ALL of D with KC float4 plane loads in flight (no LDS merge, as softargmin_wave_kernel);
+// first index on ties, NaN wins (torch.argmax / argmin), as argext_kernel.
 template <bool MAXMODE, int KC>
-__global__ __launch_bounds__(kThreads) void argext_f32x4_kernel(const float* __restrict__ vol,
-                                                                int64_t* __restrict__ out, int D,
-                                                                int W, int64_t vsn, int64_t vsd) {
-  __shared__ float sm_b[3][4][64];
-  __shared__ int sm_i[3][4][64];
+__global__ __launch_bounds__(64) void argext_wave_kernel(const float* __restrict__ vol,
+                                                         int64_t* __restrict__ out, int D, int W,
+                                                         int64_t vsn, int64_t vsd, int nunits) {
   const int P = (W + 255) >> 8;
   const int unit = blockIdx.x;
+  if (unit >= nunits) return;
   const int n = unit / P;
-  const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const int x0 = ((unit - n * P) * 64 + lane) * 4;
-  const bool any = x0 < W;
-  const int Dq = (D + 3) >> 2;
-  const int dbeg = min(D, wave * Dq);
-  const int dend = min(D, dbeg + Dq);
-  const float* base = vol + n * vsn + (any ? x0 : 0);
+  if (x0 >= W) return;
+  const float* base = vol + n * vsn + x0;
   float best[4];
   int idx[4];
   bool nanb[4];
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     best[p] = MAXMODE ? -INFINITY : INFINITY;
-    idx[p] = -1;  // -1: this quarter is empty
+    idx[p] = -1;
     nanb[p] = false;
   }
-  if (any) {
-    for (int d0 = dbeg; d0 < dend; d0 += KC) {
-      float4 v4[KC];
+  for (int d0 = 0; d0 < D; d0 += KC) {
+    float4 v4[KC];
 #pragma unroll
-      for (int k = 0; k < KC; ++k)
-        v4[k] = *reinterpret_cast<const float4*>(base + (int64_t)min(d0 + k, dend - 1) * vsd);
+    for (int k = 0; k < KC; ++k)
+      v4[k] = *reinterpret_cast<const float4*>(base + (int64_t)min(d0 + k, D - 1) * vsd);
 #pragma unroll
-      for (int k = 0; k < KC; ++k) {
-        if (d0 + k < dend) {
+    for (int k = 0; k < KC; ++k) {
+      if (d0 + k < D) {
 #pragma unroll
-          for (int p = 0; p < 4; ++p) {
-            const float v = p == 0 ? v4[k].x : p == 1 ? v4[k].y : p == 2 ? v4[k].z : v4[k].w;
-            const bool vnan = v != v;
-            const bool better = idx[p] < 0 || (MAXMODE ? (v > best[p]) : (v < best[p]));
-            if (!nanb[p] && (vnan || better)) {
-              best[p] = v;
-              idx[p] = d0 + k;
-              nanb[p] = vnan;
-            }
+        for (int p = 0; p < 4; ++p) {
+          const float v = p == 0 ? v4[k].x : p == 1 ? v4[k].y : p == 2 ? v4[k].z : v4[k].w;
+          const bool vnan = v != v;
+          const bool better = idx[p] < 0 || (MAXMODE ? (v > best[p]) : (v < best[p]));
+          if (!nanb[p] && (vnan || better)) {
+            best[p] = v;
+            idx[p] = d0 + k;
+            nanb[p] = vnan;
           }
         }
       }
     }
   }
-  if (wave != 0) {
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      sm_b[wave - 1][p][lane] = best[p];
-      sm_i[wave - 1][p][lane] = idx[p];
-    }
-  }
-  __syncthreads();
-  if (wave != 0 || !any) return;
-  long long r[4];
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    float B = best[p];
-    int I = idx[p];
-    for (int w = 0; w < 3; ++w) {  // quarters in disparity order
-      const int iw = sm_i[w][p][lane];
-      if (iw < 0) continue;
-      const float bw = sm_b[w][p][lane];
-      if (I < 0) {
-        B = bw;
-        I = iw;
-        continue;
-      }
-      if (B != B) break;  // a NaN already won
-      if ((bw != bw) || (MAXMODE ? (bw > B) : (bw < B))) {
-        B = bw;
-        I = iw;
-      }
-    }
-    r[p] = I < 0 ? 0 : I;
-  }
   int64_t* o = out + (int64_t)n * W + x0;
-  reinterpret_cast<longlong2*>(o)[0] = make_longlong2(r[0], r[1]);
-  reinterpret_cast<longlong2*>(o)[1] = make_longlong2(r[2], r[3]);
+  reinterpret_cast<longlong2*>(o)[0] = make_longlong2(idx[0] < 0 ? 0 : idx[0], idx[1] < 0 ? 0 : idx[1]);
+  reinterpret_cast<longlong2*>(o)[1] = make_longlong2(idx[2] < 0 ? 0 : idx[2], idx[3] < 0 ? 0 : idx[3]);
 }
 
 int check_vol(const void* volume, const void* out, int dtype, int64_t N, int64_t D, int64_t H,
@@ -508,11 +431,11 @@ int softargmin_entry(const void* volume, void* out, int dtype, int64_t N, int64_
     const int Wf = (int)W;
     const int64_t nunits = ceil_div(Wf, 64 * 4) * N;
     if (nunits > INT32_MAX) return fail(SM_EINVAL, "soft-argmin: too many pixels for one launch");
-    // 6 waves/SIMD (74 VGPRs); forcing 7 (72 VGPRs) or 8 (spills) measured no faster at r01
-    hipLaunchKernelGGL((softargmin_f32x4_kernel<8>), dim3((unsigned)nunits), dim3(kThreads), 0, st,
+    // one 64-lane wave per block (measured r01: 16-plane chunks or 4 waves per block no faster)
+    hipLaunchKernelGGL((softargmin_wave_kernel<8, 1>), dim3((unsigned)nunits), dim3(64), 0, st,
                        static_cast<const float*>(volume), static_cast<float*>(out), (int)D, Wf,
-                       vs.n, vs.d);
-    return check_launch("softargmin_f32x4_kernel");
+                       vs.n, vs.d, (int)nunits);
+    return check_launch("softargmin_wave_kernel");
   }
   const bool v4 = dtype == SM_F32 && (W % 4 == 0) && (vs.h % 4 == 0) && (vs.d % 4 == 0) &&
                   (vs.n % 4 == 0) && ((reinterpret_cast<uintptr_t>(volume) & 15u) == 0);
@@ -557,12 +480,12 @@ int argext_entry(const void* volume, int64_t* out, int dtype, int64_t N, int64_t
     if (nunits > INT32_MAX) return fail(SM_EINVAL, "argext: too many pixels for one launch");
     const float* v = static_cast<const float*>(volume);
     if (mode == SM_ARGMAX)
-      hipLaunchKernelGGL((argext_f32x4_kernel<true, 8>), dim3((unsigned)nunits), dim3(kThreads), 0,
-                         st, v, out, (int)D, (int)W, vs.n, vs.d);
+      hipLaunchKernelGGL((argext_wave_kernel<true, 8>), dim3((unsigned)nunits), dim3(64), 0, st, v,
+                         out, (int)D, (int)W, vs.n, vs.d, (int)nunits);
     else
-      hipLaunchKernelGGL((argext_f32x4_kernel<false, 8>), dim3((unsigned)nunits), dim3(kThreads), 0,
-                         st, v, out, (int)D, (int)W, vs.n, vs.d);
-    return check_launch("argext_f32x4_kernel");
+      hipLaunchKernelGGL((argext_wave_kernel<false, 8>), dim3((unsigned)nunits), dim3(64), 0, st, v,
+                         out, (int)D, (int)W, vs.n, vs.d, (int)nunits);
+    return check_launch("argext_wave_kernel");
   }
   dim3 grid((unsigned)ceil_div(W, 64), (unsigned)H, (unsigned)N);
   SM_DISPATCH_DTYPE(dtype, T, {
