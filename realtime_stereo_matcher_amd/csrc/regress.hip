@@ -217,7 +217,7 @@ __device__ __forceinline__ void fold_chunk(const float (&v)[KC], int nd, int d0,
 // of 4.  No LDS merge and no barrier: a one-wave block retires as soon as its wave ends (r01,
 // cfg2: 74 us vs 79 us for 4 waves splitting D with an LDS merge, and vs 105 us for the first
 // fp64-per-element kernel).  WPB waves per block work on consecutive units.
-template <int KC, int WPB>
+template <int KC, int WPB, bool PRESOFT = false>
 __global__ __launch_bounds__(64 * WPB) void softargmin_wave_kernel(const float* __restrict__ vol,
                                                                    float* __restrict__ out, int D,
                                                                    int W, int64_t vsn, int64_t vsd,
@@ -249,16 +249,22 @@ __global__ __launch_bounds__(64 * WPB) void softargmin_wave_kernel(const float* 
       float v[KC];
 #pragma unroll
       for (int k = 0; k < KC; ++k) v[k] = p == 0 ? v4[k].x : p == 1 ? v4[k].y : p == 2 ? v4[k].z : v4[k].w;
-      if (nd == KC)
+      if (PRESOFT) {  // sum_d d * v, fp64 per element as the generic kernel
+#pragma unroll
+        for (int k = 0; k < KC; ++k)
+          if (k < nd) T[p] += (double)(d0 + k) * (double)v[k];
+      } else if (nd == KC) {
         fold_chunk<KC, true>(v, nd, d0, m[p], S[p], T[p]);
-      else
+      } else {
         fold_chunk<KC, false>(v, nd, d0, m[p], S[p], T[p]);
+      }
     }
   }
   float res[4];
 #pragma unroll
   for (int p = 0; p < 4; ++p)
-    res[p] = (D == 0) ? 0.f : (m[p] == INFINITY || m[p] == -INFINITY) ? NAN : (float)(T[p] / S[p]);
+    res[p] = PRESOFT ? (float)T[p]
+             : (D == 0) ? 0.f : (m[p] == INFINITY || m[p] == -INFINITY) ? NAN : (float)(T[p] / S[p]);
   *reinterpret_cast<float4*>(out + (int64_t)n * W + x0) = make_float4(res[0], res[1], res[2], res[3]);
 }
 
@@ -424,7 +430,7 @@ int softargmin_entry(const void* volume, void* out, int dtype, int64_t N, int64_
   hipStream_t st = as_stream(stream);
   const bool presoft = flags == SM_REGRESS_PRESOFTMAXED;
   flatten_plane(vs, &H, &W);
-  const bool flat4 = dtype == SM_F32 && !presoft && (H == 1) && (W % 4 == 0) &&
+  const bool flat4 = dtype == SM_F32 && (H == 1) && (W % 4 == 0) &&
                      (vs.d % 4 == 0) && (vs.n % 4 == 0) && (H * W < (int64_t)1 << 30) &&
                      ((reinterpret_cast<uintptr_t>(volume) & 15u) == 0);
   if (flat4) {
@@ -432,9 +438,14 @@ int softargmin_entry(const void* volume, void* out, int dtype, int64_t N, int64_
     const int64_t nunits = ceil_div(Wf, 64 * 4) * N;
     if (nunits > INT32_MAX) return fail(SM_EINVAL, "soft-argmin: too many pixels for one launch");
     // one 64-lane wave per block (measured r01: 16-plane chunks or 4 waves per block no faster)
-    hipLaunchKernelGGL((softargmin_wave_kernel<8, 1>), dim3((unsigned)nunits), dim3(64), 0, st,
-                       static_cast<const float*>(volume), static_cast<float*>(out), (int)D, Wf,
-                       vs.n, vs.d, (int)nunits);
+    if (presoft)
+      hipLaunchKernelGGL((softargmin_wave_kernel<8, 1, true>), dim3((unsigned)nunits), dim3(64), 0,
+                         st, static_cast<const float*>(volume), static_cast<float*>(out), (int)D,
+                         Wf, vs.n, vs.d, (int)nunits);
+    else
+      hipLaunchKernelGGL((softargmin_wave_kernel<8, 1>), dim3((unsigned)nunits), dim3(64), 0, st,
+                         static_cast<const float*>(volume), static_cast<float*>(out), (int)D, Wf,
+                         vs.n, vs.d, (int)nunits);
     return check_launch("softargmin_wave_kernel");
   }
   const bool v4 = dtype == SM_F32 && (W % 4 == 0) && (vs.h % 4 == 0) && (vs.d % 4 == 0) &&
