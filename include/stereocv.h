@@ -47,10 +47,14 @@ enum sm_ip_algo {
   SM_IP_MFMA_F32 = 2,    /* banded C-contraction on v_mfma_f32_16x16x4_f32 (exact fp32 fma) */
   SM_IP_MFMA_BF16X3 = 3, /* banded C-contraction on bf16 MFMA over an exact 3-way bf16 split */
   /* 4: reserved (a retired warp-specialised variant of the bf16 split) */
-  SM_IP_MFMA_H2 = 5      /* default: banded contraction on 32x32x16 MFMA, two workgroups per CU;
+  SM_IP_MFMA_H2 = 5,     /* banded contraction on 32x32x16 MFMA, two workgroups per CU, every wave
+                            loads, stages, multiplies and stores (the r01 default) */
+  SM_IP_MFMA_WS = 6      /* default: the same banded contraction, one warp-specialised workgroup
+                            per CU: 4 staging waves (LDS-DMA, operand conversion) feed 4 MFMA
+                            waves (matrix work, shear, stores) through two LDS stage slots.
                             fp16 / bf16 features as they are (exact products), fp32 features as
-                            a per-segment power-of-two scaled, range-checked two-plane fp16 split
-                            (segments holding +-inf take an exact fp32 path) */
+                            a per-item power-of-two scaled, range-checked two-plane fp16 split
+                            rounded to nearest (items holding +-inf take an exact fp32 path) */
 };
 
 /* Library version (major*10000 + minor*100 + patch). */

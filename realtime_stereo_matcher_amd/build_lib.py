@@ -18,7 +18,7 @@ CSRC = os.path.join(PKG, "csrc")
 BUILD = os.path.join(ROOT, "build", "stereocv")
 LIB = os.path.join(PKG, "libstereocv.so")
 ARCH = "gfx950"
-CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", os.path.join(ROOT, "include"),
+CXXFLAGS = ["-O3", "-std=c++20", "-fPIC", f"--offload-arch={ARCH}", "-I", os.path.join(ROOT, "include"),
             "-Wall", "-Wno-unused-function", "-munsafe-fp-atomics"]
 
 
