@@ -48,9 +48,9 @@ enum sm_ip_algo {
   SM_IP_MFMA_BF16X3 = 3, /* banded C-contraction on bf16 MFMA over an exact 3-way bf16 split */
   /* 4: reserved (a retired warp-specialised variant of the bf16 split) */
   SM_IP_MFMA_H2 = 5,     /* banded contraction on 32x32x16 MFMA, two workgroups per CU, every wave
-                            loads, stages, multiplies and stores (the r01 default) */
-  SM_IP_MFMA_WS = 6      /* default: the same banded contraction, one warp-specialised workgroup
-                            per CU: 4 staging waves (LDS-DMA, operand conversion) feed 4 MFMA
+                            loads, stages, multiplies and stores (the default) */
+  SM_IP_MFMA_WS = 6      /* the same banded contraction, one warp-specialised workgroup
+                            per CU: 4 staging waves (loads, operand conversion) feed 4 MFMA
                             waves (matrix work, shear, stores) through two LDS stage slots.
                             fp16 / bf16 features as they are (exact products), fp32 features as
                             a per-item power-of-two scaled, range-checked two-plane fp16 split
@@ -142,7 +142,9 @@ int sm_cv_diff(const void* left, const void* right, void* out, int dtype,
  *                                    inline mobile_stereo_net.py:144-147)
  *   flags = SM_REGRESS_PRESOFTMAXED: sum_d d * v              (mobile_stereo_net_v4.py:10-14)
  * out: (N, H, W) in `dtype` (keepdim is a caller-side view).  fp64 accumulation.
- * vol_strides: element strides of (N, D, H, W), W stride must be 1 (NULL = contiguous). */
+ * vol_strides: element strides of (N, D, H, W), W stride must be 1 (NULL = contiguous).
+ * Any 4-byte aligned out works; fp32 planes with a 16-B aligned volume AND out take the
+ * vectorised one-wave kernel, other alignments the generic kernel (same results). */
 int sm_regress_softargmin(const void* volume, void* out, int dtype,
                           int64_t N, int64_t D, int64_t H, int64_t W, int flags,
                           const int64_t* vol_strides, void* stream);

@@ -52,6 +52,10 @@
 
 #include <type_traits>
 
+#ifndef SMCV_NT_STORE
+#define SMCV_NT_STORE 1  // volume stores non-temporal (0: plain, for A/B)
+#endif
+
 #ifndef SMCV_ABLATE
 #define SMCV_ABLATE 0  // diagnostics only (scripts/ip_stamps.hip): 1 no MFMA, 2 all feature
 #endif                 // loads from one line, 4 no stores, 8 no epilogue
@@ -201,16 +205,28 @@ template <typename T>
 __device__ __forceinline__ void store_quad(T* p, f32x4v v) {
   typedef __attribute__((address_space(1))) void gvoid;
   gvoid* g = (gvoid*)p;
+  // non-temporal: the volume is written once and never re-read by this kernel; plain stores
+  // would allocate its lines in L2 and evict the feature lines the loads reuse
+  // (scripts/micro/mlp_patterns.hip: cfg2 reads + writes 140 us plain vs 106 us nt)
   if constexpr (sizeof(T) == 4) {
-    *reinterpret_cast<__attribute__((address_space(1))) f32x4v*>(g) = v;
+    if (SMCV_NT_STORE)
+      __builtin_nontemporal_store(v, reinterpret_cast<__attribute__((address_space(1))) f32x4v*>(g));
+    else
+      *reinterpret_cast<__attribute__((address_space(1))) f32x4v*>(g) = v;
   } else if constexpr (std::is_same<T, __half>::value) {
     typedef _Float16 h4 __attribute__((ext_vector_type(4)));
     const h4 r = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
-    *reinterpret_cast<__attribute__((address_space(1))) h4*>(g) = r;
+    if (SMCV_NT_STORE)
+      __builtin_nontemporal_store(r, reinterpret_cast<__attribute__((address_space(1))) h4*>(g));
+    else
+      *reinterpret_cast<__attribute__((address_space(1))) h4*>(g) = r;
   } else {
     typedef __bf16 b4 __attribute__((ext_vector_type(4)));
     const b4 r = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
-    *reinterpret_cast<__attribute__((address_space(1))) b4*>(g) = r;
+    if (SMCV_NT_STORE)
+      __builtin_nontemporal_store(r, reinterpret_cast<__attribute__((address_space(1))) b4*>(g));
+    else
+      *reinterpret_cast<__attribute__((address_space(1))) b4*>(g) = r;
   }
 }
 template <typename T>

@@ -48,6 +48,10 @@
 #include <atomic>
 #include <type_traits>
 
+#ifndef SMCV_NT_STORE
+#define SMCV_NT_STORE 1  // volume stores non-temporal (0: plain, for A/B)
+#endif
+
 #ifndef SMCV_ABLATE
 #define SMCV_ABLATE 0  // diagnostics only (scripts/ws_ablate.hip): 1 no MFMA, 2 no fragment reads
 #endif                 // or MFMA, 4 no volume stores, 8 no shear/epilogue, 16 no staging split /
@@ -93,8 +97,6 @@ struct Geo {
   static constexpr int RW = kXT + DMAX;   // right-window rows
   static constexpr int ROWS = RW + kXT;   // + left-tile rows
   static constexpr int PLANE = ROWS * kRowB;
-  static constexpr int GROUPS = ROWS / 4; // 4-pixel groups per 8-channel chunk
-  static constexpr int ITEMS = 2 * GROUPS;
   static constexpr int STAGE = NP * PLANE;  // one stage slot
   static constexpr int NCH = TMAX - 1;      // volume chunks (32 disparities) per MFMA wave
   static constexpr int RINGW = NCH * kChunk;
@@ -103,8 +105,7 @@ struct Geo {
   static constexpr int CTRL = HDR + 2 * kHdr;     // two control records (iteration parity)
   static constexpr int DUMP = CTRL + 32;           // one word per MFMA lane (partial blocks)
   static constexpr size_t SHM = (size_t)DUMP + 4 * 64 * kMW;
-  static_assert(ITEMS <= 64 * kPW, "one staging item per staging lane");
-  static_assert(GROUPS % 8 == 0, "8-lane write groups stay inside one chunk");
+  static_assert(RW % 32 == 0 && kXT % 32 == 0, "8-lane write groups stay inside one chunk");
   static_assert(SHM <= (size_t)kLdsMax, "one workgroup per CU");
 };
 
@@ -170,10 +171,28 @@ __device__ __forceinline__ void stage_barrier() {
 template <typename T> struct Quad { using type = u32x2; };
 template <> struct Quad<float> { using type = f32x4v; };
 
+// Feature loads of the staging waves: inline asm, so that the compiler neither waits for them
+// itself (its waitcnt pass loses track of which of the two register sets is older across the
+// stage loop and drains both) nor knows them; the waves count vmcnt by hand (vm_wait: the older
+// set = all but the newer set's kLoads loads).  scripts/check_ws_asm.py replays the compiled
+// code's vector-memory queue and checks that no instruction touches a load's registers before
+// its wait.
 template <typename QT>
-__device__ __forceinline__ QT gload(const void* p) {
-  typedef __attribute__((address_space(1))) const void gcvoid;
-  return *reinterpret_cast<__attribute__((address_space(1))) const QT*>((gcvoid*)p);
+__device__ __forceinline__ void gload(QT& v, const void* p) {
+  if constexpr (sizeof(QT) == 16) {
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  } else {
+    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  }
+}
+// Wait until at most N loads of this wave are in flight; the set about to be consumed is tied.
+template <int N, typename QT>
+__device__ __forceinline__ void vm_wait(QT (&v)[kLoads]) {
+  asm volatile("s_waitcnt vmcnt(%8)"
+               : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]),
+                 "+v"(v[6]), "+v"(v[7])
+               : "n"(N)
+               : "memory");
 }
 
 // 4 fp32 results -> storage type (round to nearest even; NaN stays NaN, overflow gives inf).
@@ -181,16 +200,28 @@ template <typename T>
 __device__ __forceinline__ void store_quad(T* p, f32x4v v) {
   typedef __attribute__((address_space(1))) void gvoid;
   gvoid* g = (gvoid*)p;
+  // non-temporal: the volume is written once and never re-read by this kernel; plain stores
+  // would allocate its lines in L2 and evict the feature lines the loads reuse
+  // (scripts/micro/mlp_patterns.hip: cfg2 reads + writes 140 us plain vs 106 us nt)
   if constexpr (sizeof(T) == 4) {
-    *reinterpret_cast<__attribute__((address_space(1))) f32x4v*>(g) = v;
+    if (SMCV_NT_STORE)
+      __builtin_nontemporal_store(v, reinterpret_cast<__attribute__((address_space(1))) f32x4v*>(g));
+    else
+      *reinterpret_cast<__attribute__((address_space(1))) f32x4v*>(g) = v;
   } else if constexpr (std::is_same<T, __half>::value) {
     typedef _Float16 h4 __attribute__((ext_vector_type(4)));
     const h4 r = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
-    *reinterpret_cast<__attribute__((address_space(1))) h4*>(g) = r;
+    if (SMCV_NT_STORE)
+      __builtin_nontemporal_store(r, reinterpret_cast<__attribute__((address_space(1))) h4*>(g));
+    else
+      *reinterpret_cast<__attribute__((address_space(1))) h4*>(g) = r;
   } else {
     typedef __bf16 b4 __attribute__((ext_vector_type(4)));
     const b4 r = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
-    *reinterpret_cast<__attribute__((address_space(1))) b4*>(g) = r;
+    if (SMCV_NT_STORE)
+      __builtin_nontemporal_store(r, reinterpret_cast<__attribute__((address_space(1))) b4*>(g));
+    else
+      *reinterpret_cast<__attribute__((address_space(1))) b4*>(g) = r;
   }
 }
 template <typename T>
@@ -264,16 +295,24 @@ __global__ __launch_bounds__(kThreads, 2) void band_ws(Args args) {
 
   if (wave >= kMW) {
     // =========================================================================== staging role
-    // Lane (ch, g) owns pixel group g (4 pixels from row 4 g of the window: rows < RW are the
-    // right window, the rest the left tile) of 8-channel chunk ch.  Stage q's 8 channel rows
-    // sit in register set q % 2; they were loaded two stages earlier.
-    const int tp = tid - 64 * kMW;
+    // Every staging wave serves one tensor: waves 0 .. PR-1 the right window (rows 0 .. RW-1 of
+    // the planes), wave PR the left tile (rows RW ..).  Lane (ch, g) of a part owns pixel group g
+    // (4 pixels, plane rows prow .. prow+3) of 8-channel chunk ch.  A wave's loads are one
+    // uniform (scalar) row base + a 32-bit lane offset; the item's decode runs once per item.
+    // Stage q's 8 channel rows sit in register set q % 2; they were loaded two stages earlier.
+    constexpr int GR = G::RW / 4, GL = kXT / 4;  // pixel groups of the window / the tile
+    constexpr int PR = (2 * GR + 63) / 64;       // right-window waves
+    static_assert(PR + 1 <= kPW, "the left tile needs a staging wave of its own");
     const int pw = wave - kMW;
-    const bool active = tp < G::ITEMS;
-    const int ch = min(tp / G::GROUPS, 1);                  // 8-channel chunk
-    const int g = min(tp - ch * G::GROUPS, G::GROUPS - 1);  // rows 4g .. 4g+3
-    const bool isR = 4 * g < G::RW;
-    const int64_t cs = isR ? rs.c : ls.c;
+    const bool isR = pw < PR;  // uniform
+    const int tr = isR ? 64 * pw + lane : lane;
+    const int gcnt = isR ? GR : GL;
+    const bool active = (isR || pw == PR) && tr < 2 * gcnt;
+    const int ch = min(tr / gcnt, 1);                  // 8-channel chunk
+    const int g = min(tr - ch * gcnt, gcnt - 1);       // pixel group
+    const int prow = (isR ? 0 : G::RW) + 4 * g;        // plane row of the group's first pixel
+    const Strides4 ts = isR ? rs : ls;                 // uniform
+    const T* tbase = isR ? R : L;
     const bool cfull = rfl(cpg % kKC) == 0;  // uniform: a scalar branch
 
     using QT = typename Quad<T>::type;
@@ -282,38 +321,49 @@ __global__ __launch_bounds__(kThreads, 2) void band_ws(Args args) {
       int nv;      // valid channels of v (0: pixels outside the image, an idle lane)
       int it, ks;  // the stage held (item -1: past the last item)
     };
-    Set st[2];
+    Set st[1];
     int cit = 0, cks = 0;  // cursor: the next stage to load
+    // the cursor item's row: uniform base (elements) and this lane's pixel offset
+    const T* ibase = tbase;
+    int ipx = 0;
+    bool iok = false;
+    // the cursor's stage into set s: exactly kLoads loads per wave and stage, on every path (past
+    // the last item and in a wave with no lanes to stage: reloads of a row start) -- the count
+    // vm_wait relies on
     auto load = [&](Set& s) {
+      cit = rfl(cit);  // wave-uniform control (scalar branches only, no exec-masked paths)
+      cks = rfl(cks);
       s.it = cit;
       s.ks = cks;
       s.nv = 0;
+      const T* q = tbase;
+      int lim = 0;
       if (cit >= 0) {
-        const Work k = decode(witem(cit), args, DMAX);
-        const int cl = cks * kKC + 8 * ch;  // channel within the group
-        const int px = isR ? k.js + 4 * g : k.x0 + 4 * g - G::RW;
-        const bool okp = active && px >= 0 && px < W;
-        const T* p = (isR ? R + (int64_t)k.n * rs.n + (int64_t)k.y * rs.h
-                          : L + (int64_t)k.n * ls.n + (int64_t)k.y * ls.h) +
-                     (okp ? px : 0) + ((int64_t)k.g * cpg + min(cl, cpg - 1)) * cs;
-        s.nv = okp ? min(max(cpg - cl, 0), 8) : 0;
-        // channel tail: clamp to the group's last channel (put() zeroes the tail)
-        const int lim = cfull ? 7 : min(max(cpg - 1 - cl, 0), 7);
-        if (active && !(SMCV_ABLATE & 32)) {
-          // each address opaque to the compiler: a clamped channel repeats the previous address,
-          // and a load the compiler merged into a register copy would wait for the load (vmcnt)
-          // right there instead of two stages later
-#pragma unroll
-          for (int kk = 0; kk < kLoads; ++kk) {
-            const T* q = p;
-            asm volatile("" : "+v"(q));
-            s.v[kk] = gload<QT>(q);
-            p = kk < lim ? p + cs : p;
-          }
+        if (cks == 0) {  // a new item: its row base and this lane's pixels
+          const Work k = decode(witem(cit), args, DMAX);
+          ibase = tbase + (int64_t)k.n * ts.n + (int64_t)k.y * ts.h + (int64_t)k.g * cpg * ts.c;
+          const int px = (isR ? k.js : k.x0) + 4 * g;
+          iok = active && px >= 0 && px < W;
+          ipx = iok ? px : 0;
         }
+        const int cl = cks * kKC + 8 * ch;  // channel within the group
+        s.nv = iok ? min(max(cpg - cl, 0), 8) : 0;
+        // channel tail: clamp to the group's last channel (put() zeroes the tail)
+        lim = cfull ? 7 : min(max(cpg - 1 - cl, 0), 7);
+        q = ibase + (int64_t)min(cl, cpg - 1) * ts.c + ipx;
         if (++cks == nks) {
           cks = 0;
           if (++cit >= nitems) cit = -1;
+        }
+      }
+      if constexpr (!(SMCV_ABLATE & 32)) {
+        // the channel stride, opaque here: the 8 addresses are stepped, not 8 hoisted offsets
+        int64_t csl = ts.c;
+        asm volatile("" : "+v"(csl));
+#pragma unroll
+        for (int kk = 0; kk < kLoads; ++kk) {
+          gload(s.v[kk], q);
+          if (kk < lim) q += csl;
         }
       }
     };
@@ -324,11 +374,11 @@ __global__ __launch_bounds__(kThreads, 2) void band_ws(Args args) {
     // register set s -> operand plane(s) of stage slot sp + its header
     auto put = [&](Set& s, int sp) {
       const unsigned hb = hdr0 + (unsigned)(sp * kHdr);
-      if (s.it < 0) {
-        if (tp == 0) *lds_int(hb + 4 * hIt) = -1;
+      if (rfl(s.it) < 0) {
+        if (pw == 0 && lane == 0) *lds_int(hb + 4 * hIt) = -1;
         return;
       }
-      if (s.ks == 0) {
+      if (rfl(s.ks) == 0) {
         kiL = kcL;
         kiR = kcR;
         mx = 0.f;
@@ -369,7 +419,7 @@ __global__ __launch_bounds__(kThreads, 2) void band_ws(Args args) {
                 ph[qq] = __builtin_bit_cast(unsigned, hv);
                 pm[qq] = __builtin_bit_cast(unsigned, mv);
               }
-              const int off = swz(4 * g + p, ch);
+              const int off = swz(prow + p, ch);
               *reinterpret_cast<uint4*>(base + off) = wh;
               *reinterpret_cast<uint4*>(base + G::PLANE + off) = wm;
             }
@@ -399,66 +449,70 @@ __global__ __launch_bounds__(kThreads, 2) void band_ws(Args args) {
               const unsigned hi = p < 2 ? qv[2 * j + 1].x : qv[2 * j + 1].y;
               pwd[j] = __builtin_amdgcn_perm(hi, lo, (p & 1) ? 0x07060302u : 0x05040100u);
             }
-            *reinterpret_cast<uint4*>(base + swz(4 * g + p, ch)) = w;
+            *reinterpret_cast<uint4*>(base + swz(prow + p, ch)) = w;
           }
         }
       }
-      if (tp == 0) {
+      if (pw == 0 && lane == 0) {
         *lds_int(hb + 4 * hIt) = s.it;
         *lds_int(hb + 4 * hKs) = s.ks;
         *lds_int(hb + 4 * hKL) = kiL;
         *lds_int(hb + 4 * hKR) = kiR;
       }
       if constexpr (NP == 2) {
-        if (s.ks == nks - 1) {  // the item's maxima, per staging wave
-          const float ml = wave_max(isR ? 0.f : mx), mr = wave_max(isR ? mx : 0.f);
+        if (rfl(s.ks) == nks - 1) {  // the item's maxima, per staging wave
+          const float m = wave_max(mx);  // a wave stages one tensor
           if (lane == 0) {
-            *lds_int(hb + 4 * (hMaxL + pw)) = __float_as_int(ml);
-            *lds_int(hb + 4 * (hMaxR + pw)) = __float_as_int(mr);
+            *lds_int(hb + 4 * (hMaxL + pw)) = __float_as_int(isR ? 0.f : m);
+            *lds_int(hb + 4 * (hMaxR + pw)) = __float_as_int(isR ? m : 0.f);
           }
         }
       }
     };
 
-    // prologue: stages 0 and 1 in flight, stage 0 into slot 0, stage 2's loads issued
-    load(st[0]);
-    load(st[1]);
-    put(st[0], 0);
-    bool ended = st[0].it < 0;
-    load(st[0]);
+    // One register set: stage q's loads are issued right after stage q-1 was staged, so they
+    // have a whole stage iteration (the MFMA waves' matrix work and stores) to land.  The loop
+    // has ONE load site (a second one, e.g. for a restage, makes the register allocator move the
+    // set between load sites, i.e. copy registers whose loads have not landed).
+    Set& cs_ = st[0];
+    // prologue: stage 0 into slot 0 (landed before the loop: no load in flight at its entry)
+    load(cs_);
+    vm_wait<0>(cs_.v);
+    put(cs_, 0);
+    bool ended = rfl(cs_.it) < 0;
     int gseen = 0;  // control generation seen
     int par = 0;    // iteration parity (control record read this iteration)
-    // iteration s writes stage s+1 into slot (s+1) % 2 from register set (s+1) % 2
-    auto pstep = [&](auto J) -> bool {
-      constexpr int j = decltype(J)::value;
+    int sp = 1;     // slot written this iteration
+    // iteration s writes stage s+1 into slot (s+1) % 2.  A restage request: the stage in flight
+    // is dropped (nothing is staged this iteration; the MFMA waves skip two iterations) and the
+    // cursor restarts at the item's first stage.
+    for (;;) {
+      load(cs_);  // the next stage (after a restage: the wrong one, dropped below)
       SM_STAMP(6);
       stage_barrier();
       SM_STAMP(3);
       const unsigned cb = ctrl0 + (unsigned)(16 * par);
       par ^= 1;
       const int gen = rfl(*lds_int(cb));
-      if (gen > gseen) {
-        // restage an item from its first stage with new scales: reload both sets
+      const bool restage = gen > gseen;
+      if (restage) {
         gseen = gen;
         kcL = rfl(*lds_int(cb + 8));
         kcR = rfl(*lds_int(cb + 12));
         cit = rfl(*lds_int(cb + 4));
         cks = 0;
-        load(st[j]);
-        load(st[j ^ 1]);
-      } else if (ended) {
-        return true;
       }
+      // every path from the load reaches this wait: the set is live (not reusable) in between
+      vm_wait<0>(cs_.v);  // this wave's only vector-memory operations are these loads
+      if (!restage && ended) break;
+      ended = ended && !restage;
       SM_STAMP(4);
-      put(st[j], j);
-      ended = st[j].it < 0;
+      if (!restage) {
+        put(cs_, sp);
+        ended = rfl(cs_.it) < 0;
+      }
       SM_STAMP(5);
-      load(st[j]);
-      return false;
-    };
-    for (;;) {
-      if (pstep(IC<1>{})) break;
-      if (pstep(IC<0>{})) break;
+      sp ^= 1;
     }
     SM_STAMP_FLUSH
     return;
@@ -783,6 +837,7 @@ __global__ __launch_bounds__(kThreads, 2) void band_ws(Args args) {
   int gseen = 0;
   int sp = 0, par = 0;
   int retried = -1;  // the item last sent back for restaging (a second failure takes the slow path)
+  int mskip = 0;     // iterations still to skip after a restage request
   for (;;) {
     SM_STAMP(2);
     stage_barrier();
@@ -790,8 +845,12 @@ __global__ __launch_bounds__(kThreads, 2) void band_ws(Args args) {
     const unsigned cb = ctrl0 + (unsigned)(16 * par);
     par ^= 1;
     const int gen = rfl(*lds_int(cb));
-    if (gen > gseen) {  // this slot was staged before a restage request: skip it
+    if (gen > gseen) {  // a restage request: this slot and the next were not staged for it
       gseen = gen;
+      mskip = 2;
+    }
+    if (mskip > 0) {
+      --mskip;
       sp ^= 1;
       continue;
     }
@@ -929,7 +988,9 @@ int ws_prepare(const void* left, const void* right, const void* out, int dtype, 
          rs.n % 4 == 0 && rs.c % 4 == 0 && rs.h % 4 == 0 &&
          ((reinterpret_cast<uintptr_t>(left) | reinterpret_cast<uintptr_t>(right)) % align == 0) &&
          reinterpret_cast<uintptr_t>(out) % 16 == 0 && 8 * H * W < INT32_MAX &&
-         8 * W * std::max<int64_t>(D, 1) < INT32_MAX;
+         8 * W * std::max<int64_t>(D, 1) < INT32_MAX &&
+         // the staging lanes' 32-bit byte offsets: pixels + up to 15 channel rows
+         (16 * std::max(ls.c, rs.c) + W) * elem_size(dtype) < INT32_MAX;
   // D passes of at most 192 disparities, balanced (D = 256: two passes of 128); a pass width
   // that is a multiple of 4 keeps every right-window pixel group aligned
   const int64_t npass = ceil_div(std::max<int64_t>(D, 1), (int64_t)192);

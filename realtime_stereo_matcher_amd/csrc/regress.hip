@@ -432,7 +432,8 @@ int softargmin_entry(const void* volume, void* out, int dtype, int64_t N, int64_
   flatten_plane(vs, &H, &W);
   const bool flat4 = dtype == SM_F32 && (H == 1) && (W % 4 == 0) &&
                      (vs.d % 4 == 0) && (vs.n % 4 == 0) && (H * W < (int64_t)1 << 30) &&
-                     ((reinterpret_cast<uintptr_t>(volume) & 15u) == 0);
+                     ((reinterpret_cast<uintptr_t>(volume) & 15u) == 0) &&
+                     ((reinterpret_cast<uintptr_t>(out) & 15u) == 0);  // float4 stores
   if (flat4) {
     const int Wf = (int)W;
     const int64_t nunits = ceil_div(Wf, 64 * 4) * N;
