@@ -19,8 +19,11 @@ class TorchGroupwiseCost(nn.Module):
         self.max_disparity = max_disparity
 
     def groupwise(self, left, right, n_groups):
-        """Zero-disparity group-wise mean, (N, G, H, W) -- the reference helper (:12-22)."""
-        return F.groupwise_volume(left, right, n_groups, 1)[..., 0]
+        """Zero-disparity group-wise mean, (N, G, H, W) in the input dtype -- the reference
+        helper (:12-22), whose (left*right).view(...).mean(2) keeps left.dtype.  The kernel
+        accumulates in fp32 and rounds once to that dtype (the reference rounds every product
+        and the mean in fp16/bf16: within its last-bit rounding)."""
+        return F.groupwise_volume(left, right, n_groups, 1)[..., 0].to(left.dtype)
 
     def forward(self, left, right):
         return F.groupwise_volume(left, right, self.n_groups, self.max_disparity)

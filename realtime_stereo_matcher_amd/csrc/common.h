@@ -7,6 +7,7 @@
 #include <hip/hip_bf16.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <string>
 
 #include "../../include/stereocv.h"
@@ -66,6 +67,16 @@ int read_strides(const int64_t* s, int64_t C, int64_t H, int64_t W, Strides4* ou
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// ------------------------------------------------------------------------------- launches
+// The device a stream belongs to (the current device for the null stream or on error).
+int stream_device(hipStream_t st);
+// Compute units of a device, cached per device (atomics: concurrent callers are safe).
+int device_cus(int dev);
+// Raise `kern`'s dynamic-LDS limit to `shm` bytes on `dev`, once per (kernel, device): `done`
+// is the kernel's own bitmask of devices already raised.  The attribute applies to the
+// current device, so it is switched to `dev` for the call and restored.
+int ensure_lds_limit(const void* kern, int shm, int dev, std::atomic<unsigned long long>& done);
 
 
 // Diagnostic phase stamps (scripts/ip_stamps.hip builds this file with -DSMCV_STAMPS; the

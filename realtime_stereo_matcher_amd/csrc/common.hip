@@ -23,6 +23,42 @@ int check_launch(const char* what) {
   return SM_OK;
 }
 
+int stream_device(hipStream_t st) {
+  int dev = 0;
+  if (st == nullptr || hipStreamGetDevice(st, &dev) != hipSuccess) {
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  }
+  return dev;
+}
+
+namespace {
+std::atomic<int> g_cus[64];
+}
+
+int device_cus(int dev) {
+  if (dev < 0 || dev >= 64) return 256;
+  int n = g_cus[dev].load(std::memory_order_relaxed);
+  if (n > 0) return n;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+    n = 256;
+  g_cus[dev].store(n, std::memory_order_relaxed);
+  return n;
+}
+
+int ensure_lds_limit(const void* kern, int shm, int dev, std::atomic<unsigned long long>& done) {
+  const unsigned long long bit = 1ull << (dev & 63);
+  if (done.load(std::memory_order_acquire) & bit) return SM_OK;
+  int cur = dev;
+  if (hipGetDevice(&cur) != hipSuccess) cur = dev;
+  if (cur != dev && hipSetDevice(dev) != hipSuccess) return fail(SM_ELAUNCH, "hipSetDevice failed");
+  const hipError_t e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, shm);
+  if (cur != dev) (void)hipSetDevice(cur);
+  if (e != hipSuccess)
+    return fail(SM_ELAUNCH, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
+  done.fetch_or(bit, std::memory_order_acq_rel);
+  return SM_OK;
+}
+
 int read_strides(const int64_t* s, int64_t C, int64_t H, int64_t W, Strides4* out,
                  const char* name) {
   if (s == nullptr) {

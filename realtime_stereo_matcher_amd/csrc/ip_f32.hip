@@ -300,19 +300,6 @@ __global__ __launch_bounds__(kThreads, 1) void ip_band_f32(
   SM_STAMP_FLUSH
 }
 
-int device_cus() {
-  static int cached[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (cached[dev] == 0) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-    cached[dev] = n;
-  }
-  return cached[dev];
-}
-
 template <int TMAX>
 int launch(const float* l, const float* r, float* o, int64_t N, int64_t C, int64_t H, int64_t W,
            int64_t D, Strides4 ls, Strides4 rs, bool mean, hipStream_t st) {
@@ -322,11 +309,11 @@ int launch(const float* l, const float* r, float* o, int64_t N, int64_t C, int64
   const int64_t nwork = (int64_t)tiles * H * N * npass;
   if (nwork > INT32_MAX) return fail(SM_EINVAL, "inner product: too much work for one launch");
   auto kern = mean ? ip_band_f32<TMAX, true> : ip_band_f32<TMAX, false>;
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::SHM);
-  if (e != hipSuccess)
-    return fail(SM_ELAUNCH, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
-  int64_t nwg = std::min<int64_t>(nwork, (int64_t)device_cus());
+  static std::atomic<unsigned long long> lds_done[2];
+  const int dev = stream_device(st);
+  if (int rc = ensure_lds_limit(reinterpret_cast<const void*>(kern), (int)G::SHM, dev, lds_done[mean]))
+    return rc;
+  int64_t nwg = std::min<int64_t>(nwork, (int64_t)device_cus(dev));
   nwg = std::max<int64_t>(8, (nwg + 7) / 8 * 8);
   hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(kThreads), G::SHM, st, l, r, o, (int)C,
                      (int)H, (int)W, (int)D, ls, rs, tiles, npass, (int)nwork);

@@ -15,10 +15,10 @@
 //
 // Operands.  fp16 / bf16 features are staged as they are (one plane; their products are exact
 // in fp32: one MFMA per block and 16-channel step).  fp32 features are scaled by a per-segment
-// power of two 2^k (exact) and split into two fp16 planes by round-toward-zero:
-// h = rtz16(x 2^k), m = rtz16(x 2^k - h), so x 2^k = h + m + e with |e| < 2^-20 |x 2^k|
-// (+ 2^-24 absolute below the fp16 normal range); the products h*h' + h*m' + m*h' (exact in
-// fp32; the dropped m*m', h*e', e*h' are each below 2^-20 relative) accumulate in fp32, and
+// power of two 2^k (exact) and split into two fp16 planes by round-to-nearest:
+// h = rn16(x 2^k), m = rn16(x 2^k - h), so x 2^k = h + m + e with |e| <= 2^-22 |x 2^k|
+// (+ 2^-25 absolute below the fp16 normal range); the products h*h' + h*m' + m*h' (exact in
+// fp32; the dropped m*m', h*e', e*h' are each at most 2^-22 relative) accumulate in fp32, and
 // the result is multiplied back by 2^-(kL+kR) (ldexp, exact).  Integer features are exact.
 //
 // Scale control (fp32).  Every lane tracks max|x| of the values it stages; at the end of a
@@ -69,7 +69,7 @@ namespace h2band {
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef __fp16 hp2 __attribute__((ext_vector_type(2)));
+typedef _Float16 hp2 __attribute__((ext_vector_type(2)));
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
@@ -398,10 +398,12 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
             const float a = col[p][2 * qq], b = col[p][2 * qq + 1];
             const float as = decltype(scaled)::value ? a * sc : a;
             const float bs = decltype(scaled)::value ? b * sc : b;
-            const hp2 hv = __builtin_amdgcn_cvt_pkrtz(as, bs);
-            const float ra = __builtin_fmaf(a, sc, -(float)hv[0]);
-            const float rb = __builtin_fmaf(b, sc, -(float)hv[1]);
-            const hp2 mv = __builtin_amdgcn_cvt_pkrtz(ra, rb);
+            const hp2 hv = {(_Float16)as, (_Float16)bs};  // v_cvt_pk_f16_f32: nearest even
+            const float ra = decltype(scaled)::value ? __builtin_fmaf(a, sc, -(float)hv[0])
+                                                     : a - (float)hv[0];
+            const float rb = decltype(scaled)::value ? __builtin_fmaf(b, sc, -(float)hv[1])
+                                                     : b - (float)hv[1];
+            const hp2 mv = {(_Float16)ra, (_Float16)rb};
             ph[qq] = __builtin_bit_cast(unsigned, hv);
             pm[qq] = __builtin_bit_cast(unsigned, mv);
           }
@@ -882,20 +884,6 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
   SM_STAMP_FLUSH
 }
 
-int device_cus() {
-  static int cached[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (cached[dev] == 0) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        n <= 0)
-      n = 256;
-    cached[dev] = n;
-  }
-  return cached[dev];
-}
-
 template <typename T, typename TO, int TMAX, bool MEAN, int LAYOUT, bool FUSE>
 int launch(Args a, int64_t N, hipStream_t st) {
   using G = Geo<T, TMAX>;
@@ -904,11 +892,11 @@ int launch(Args a, int64_t N, hipStream_t st) {
   if (nwork > INT32_MAX / 64) return fail(SM_EINVAL, "band kernel: too much work for one launch");
   a.nwork = (int)nwork;
   auto kern = band_h2<T, TO, TMAX, MEAN, LAYOUT, FUSE>;
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::SHM);
-  if (e != hipSuccess)
-    return fail(SM_ELAUNCH, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
-  int64_t nwg = std::min<int64_t>(nwork, wg_per_cu<FUSE>() * (int64_t)device_cus());
+  static std::atomic<unsigned long long> lds_done{0};  // per instantiation
+  const int dev = stream_device(st);
+  if (int rc = ensure_lds_limit(reinterpret_cast<const void*>(kern), (int)G::SHM, dev, lds_done))
+    return rc;
+  int64_t nwg = std::min<int64_t>(nwork, wg_per_cu<FUSE>() * (int64_t)device_cus(dev));
   nwg = std::max<int64_t>(8, (nwg + 7) / 8 * 8);
   hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(kThreads), G::SHM, st, a);
   return check_launch("band_h2");

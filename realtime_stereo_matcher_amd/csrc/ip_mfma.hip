@@ -560,19 +560,6 @@ int ablate_bits() {
   return e ? atoi(e) : 0;
 }
 
-int device_cus() {
-  static int cached[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (cached[dev] == 0) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-    cached[dev] = n;
-  }
-  return cached[dev];
-}
-
 template <typename T, int P, int TMAX>
 int launch_band(const void* l, const void* r, void* o, int64_t N, int64_t C, int64_t H, int64_t W,
                 int64_t D, Strides4 ls, Strides4 rs, int divisor, hipStream_t st) {
@@ -595,12 +582,13 @@ int launch_band(const void* l, const void* r, void* o, int64_t N, int64_t C, int
   const bool mean = divisor >= 0;
   auto kern = vec ? (mean ? ip_band_mfma<T, P, TMAX, true, true> : ip_band_mfma<T, P, TMAX, true, false>)
                   : (mean ? ip_band_mfma<T, P, TMAX, false, true> : ip_band_mfma<T, P, TMAX, false, false>);
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-  if (e != hipSuccess)
-    return fail(SM_ELAUNCH, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
+  static std::atomic<unsigned long long> lds_done[4];
+  const int dev = stream_device(st);
+  if (int rc = ensure_lds_limit(reinterpret_cast<const void*>(kern), (int)shm, dev,
+                                lds_done[2 * vec + mean]))
+    return rc;
   // persistent grid: one 8-wave workgroup per CU (LDS-limited), a multiple of 8
-  int64_t nwg = std::min<int64_t>(nwork, (int64_t)device_cus());
+  int64_t nwg = std::min<int64_t>(nwork, (int64_t)device_cus(dev));
   nwg = std::max<int64_t>(8, (nwg + 7) / 8 * 8);
   hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(kThreads), shm, st, static_cast<const T*>(l),
                      static_cast<const T*>(r), static_cast<T*>(o), (int)C, (int)H, (int)W, (int)D,

@@ -918,21 +918,6 @@ __global__ __launch_bounds__(kThreads, 2) void band_ws(Args args) {
   SM_STAMP_FLUSH
 }
 
-std::atomic<int> g_cus[64];
-
-// compute units of the stream's device (cached per device; atomics: no data race)
-int device_cus(hipStream_t st) {
-  int dev = 0;
-  if (hipStreamGetDevice(st, &dev) != hipSuccess && hipGetDevice(&dev) != hipSuccess) return 256;
-  if (dev < 0 || dev >= 64) return 256;
-  int n = g_cus[dev].load(std::memory_order_relaxed);
-  if (n > 0) return n;
-  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-    n = 256;
-  g_cus[dev].store(n, std::memory_order_relaxed);
-  return n;
-}
-
 template <typename T, typename TO, int TMAX, bool MEAN, int LAYOUT, bool FUSE>
 int launch(Args a, int64_t N, hipStream_t st) {
   using G = Geo<T, TMAX>;
@@ -941,19 +926,11 @@ int launch(Args a, int64_t N, hipStream_t st) {
   if (nwork > INT32_MAX / 64) return fail(SM_EINVAL, "band kernel: too much work for one launch");
   a.nwork = (int)nwork;
   auto kern = band_ws<T, TO, TMAX, MEAN, LAYOUT, FUSE>;
-  // the dynamic-LDS limit, raised once per instantiation and device
-  static std::atomic<unsigned long long> attr_set{0};
-  int dev = 0;
-  if (hipStreamGetDevice(st, &dev) != hipSuccess) (void)hipGetDevice(&dev);
-  const unsigned long long bit = 1ull << (dev & 63);
-  if ((attr_set.load(std::memory_order_acquire) & bit) == 0) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::SHM);
-    if (e != hipSuccess)
-      return fail(SM_ELAUNCH, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
-    attr_set.fetch_or(bit, std::memory_order_acq_rel);
-  }
-  int64_t nwg = std::min<int64_t>(nwork, (int64_t)device_cus(st));
+  static std::atomic<unsigned long long> lds_done{0};  // per instantiation
+  const int dev = stream_device(st);
+  if (int rc = ensure_lds_limit(reinterpret_cast<const void*>(kern), (int)G::SHM, dev, lds_done))
+    return rc;
+  int64_t nwg = std::min<int64_t>(nwork, (int64_t)device_cus(dev));
   nwg = std::max<int64_t>(8, (nwg + 7) / 8 * 8);
   hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(kThreads), G::SHM, st, a);
   return check_launch("band_ws");

@@ -107,9 +107,12 @@ class _ForwardOnly(torch.autograd.Function):
 
 
 def _run(fn, *inputs):
-    if torch.is_grad_enabled() and any(t.requires_grad for t in inputs):
-        return _ForwardOnly.apply(fn, *inputs)
-    return fn()
+    # the entry points size persistent grids and set kernel attributes on the CURRENT HIP
+    # device: make it the inputs' device for the call
+    with torch.cuda.device(inputs[0].device):
+        if torch.is_grad_enabled() and any(t.requires_grad for t in inputs):
+            return _ForwardOnly.apply(fn, *inputs)
+        return fn()
 
 
 def _ptr(t):

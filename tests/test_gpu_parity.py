@@ -201,7 +201,7 @@ def test_inner_product_vs_oracle(shape, algo):
     n, c, h, w, D = shape
     l, r = _feats(hash(shape) % 1000, (n, c, h, w))
     got = host(F.inner_product_volume(dev(l), dev(r), D, algo=algo))
-    np.testing.assert_allclose(got, O.inner_product(l, r, D), atol=TOL * max(1, c / 64), rtol=0)
+    np.testing.assert_allclose(got, O.inner_product(l, r, D), atol=TOL, rtol=0)
     li, ri = _feats(7, (n, c, h, w), "int")
     np.testing.assert_array_equal(host(F.inner_product_volume(dev(li), dev(ri), D, algo=algo)),
                                   O.inner_product(li, ri, D))
@@ -404,6 +404,39 @@ def test_regression_special_values_flat(W):
     np.testing.assert_array_equal(host(F.hard_argmin(dev(vt))), torch.argmin(torch.from_numpy(vt), 1).numpy())
 
 
+@pytest.mark.parametrize("hw", [(2, 8), (3, 5)])  # H*W % 4 == 0: the flat fp32 kernel; else generic
+@pytest.mark.parametrize("D", [37, 48])
+def test_regression_presoftmax_special_values(hw, D):
+    """The v4 regression over already-softmaxed input (model/mobile_stereo_net_v4.py:10-14) on
+    the flat one-wave kernel and its generic twin: inf * 0 at d = 0 gives NaN (torch), a NaN entry
+    propagates, +inf elsewhere gives inf, D % 8 != 0 leaves a partial chunk -- against
+    torch.sum(x * arange(D)) on the CPU, and flat vs generic agree."""
+    from realtime_stereo_matcher_amd import functional as F
+
+    H, W = hw
+    x = np.random.default_rng(6).random((2, D, H, W)).astype(np.float32)
+    x /= x.sum(1, keepdims=True)
+    x[0, 0, 0, 0] = np.inf                       # inf * 0 -> NaN
+    x[0, 5, 0, 1] = np.nan                       # NaN propagates
+    x[1, D - 1, H - 1, W - 1] = np.inf           # inf * (D - 1) -> inf
+    x[1, 3, 0, 2] = -np.inf
+    x[1, 9, 0, 2] = np.inf                       # -inf and +inf -> NaN
+    t = torch.from_numpy(x)
+    ref = torch.sum(t * torch.arange(D, dtype=torch.float32).view(1, -1, 1, 1), 1).numpy()
+    got = host(F.regression_presoftmax(dev(x)))
+    np.testing.assert_array_equal(np.isnan(got), np.isnan(ref))
+    np.testing.assert_array_equal(np.isinf(got), np.isinf(ref))
+    fin = np.isfinite(ref)
+    np.testing.assert_allclose(got[fin], ref[fin], atol=TOL, rtol=1e-6)
+    # the same planes at a 4-byte (not 16-byte) aligned offset take the generic kernel
+    big = torch.zeros(2 * D * H * W + 1, device="cuda")
+    xs = big[1:].view(2, D, H, W)
+    xs.copy_(dev(x))
+    got2 = host(F.regression_presoftmax(xs))
+    np.testing.assert_array_equal(np.isnan(got2), np.isnan(got))
+    np.testing.assert_allclose(got2[fin], got[fin], atol=TOL, rtol=1e-6)
+
+
 def test_zero_channels_and_empty():
     from realtime_stereo_matcher_amd import functional as F
 
@@ -443,8 +476,11 @@ def test_cfg2_inner_product_full_size(algo):
     vol = F.inner_product_volume(L, R, 192, algo=algo)
     disp = F.soft_argmin(vol)
     torch.cuda.synchronize()
+    from oracle.torch_port import soft_argmin_eager, sweep_dot_volume
+
     ln, rn = host(L), host(R)
     rng = np.random.default_rng(3)
+    worst = worst_torch = 0.0
     for y in (0, 1, 269, 538, 539):
         ref = O.inner_product(ln[:, :, y:y + 1], rn[:, :, y:y + 1], 192)
         got_v = host(vol[:, :, y:y + 1])
@@ -452,13 +488,24 @@ def test_cfg2_inner_product_full_size(algo):
         # the regression kernel on this volume vs the fp64 regression of the same volume
         got_d = host(disp[:, :, y:y + 1])
         np.testing.assert_allclose(got_d, O.softargmin(got_v), atol=TOL, rtol=0)
-        # end to end: fp32-volume rounding is amplified by sharp / bimodal softmaxes for a few
-        # pixels (torch's own fp32 path has the same sensitivity), so the bar is the north
-        # star's DISPARITY EPE: mean |disp - gt| identical to the exact pipeline within 1e-4.
+        # end to end, per pixel: |disp - fp64 pipeline| against the same deviation of torch's
+        # own fp32 pipeline (the reference's arithmetic) on these rows.  fp32-volume rounding is
+        # amplified by sharp / bimodal softmaxes at a few pixels, for torch as for the kernel
+        # (same amplification, different rounding), so the bar is max(1e-4, 2x the torch-fp32
+        # deviation) over the sampled rows; the EPE against any ground truth then differs from
+        # the exact pipeline's by at most that.
+        exact = O.softargmin(ref).astype(np.float64)
+        t32 = soft_argmin_eager(sweep_dot_volume(torch.from_numpy(ln[:, :, y:y + 1]),
+                                                 torch.from_numpy(rn[:, :, y:y + 1]), 192))
+        worst_torch = max(worst_torch, np.abs(t32.numpy().astype(np.float64) - exact).max())
+        worst = max(worst, np.abs(got_d.astype(np.float64) - exact).max())
         gt = rng.uniform(0, 191, size=got_d.shape)
         epe_kernel = np.abs(got_d - gt).mean()
-        epe_exact = np.abs(O.softargmin(ref).astype(np.float64) - gt).mean()
+        epe_exact = np.abs(exact - gt).mean()
         assert abs(epe_kernel - epe_exact) <= TOL, (epe_kernel, epe_exact)
+    print(f"cfg2 {algo}: max per-pixel |disp - fp64 pipeline|: kernel {worst:.3g}, "
+          f"torch fp32 {worst_torch:.3g}")
+    assert worst <= max(TOL, 2 * worst_torch), (worst, worst_torch)
     # x < d triangle is exactly zero everywhere
     tri = torch.arange(960, device="cuda")[None, :] < torch.arange(192, device="cuda")[:, None]
     assert not vol[0].permute(1, 0, 2)[:, tri].any()
@@ -514,11 +561,16 @@ def test_cfg5_concat_interweave_fp16_full_size():
         assert torch.equal(vol[0, :128, :, d:, d], L[0, :, :, d:])
         assert torch.equal(vol[0, 128:, :, d:, d], R[0, :, :, :960 - d])
     del vol
-    sv = F.interweave_volume(L[:, :16], R[:, :16], 64)
-    for d in (0, 5, 63):
-        assert torch.equal(sv[0, 0::2, d, :, d:], L[0, :16, :, d:])
-        assert torch.equal(sv[0, 1::2, d, :, d:], R[0, :16, :, :960 - d])
+    # the v4 shifted interweave at the full C = 128 (a 17 GB volume): every d slice
+    sv = F.interweave_volume(L, R, 64)
+    assert sv.shape == (1, 256, 64, 540, 960)
+    for d in range(64):
+        assert torch.equal(sv[0, 0::2, d, :, d:], L[0, :, :, d:])
+        assert torch.equal(sv[0, 1::2, d, :, d:], R[0, :, :, :960 - d])
         assert not sv[0, :, d, :, :d].any()
+    for y in (0, 539):
+        np.testing.assert_array_equal(host(sv[:, :, :, y:y + 1]),
+                                      O.interweave_shifted(ln[:, :, y:y + 1], rn[:, :, y:y + 1], 64))
 
 
 # =============================================================================== band kernel: groupwise + fused
