@@ -7,8 +7,9 @@
  *
  *   - Pointers are DEVICE pointers (HIP).  The library never allocates, frees or
  *     synchronises caller memory; all work is enqueued on `stream` (a hipStream_t
- *     passed as void*, NULL = the null stream) and is stream-ordered.  No host sync,
- *     no global mutable state except the thread-local error string.
+ *     passed as void*, NULL = the null stream) and is stream-ordered.  No host sync;
+ *     the only state besides the thread-local error string is a per-device cache
+ *     (atomics) of the CU count and of the kernels whose LDS limit was raised.
  *   - Feature maps are 4-D (N, C, H, W).  `l_strides` / `r_strides` give the element
  *     strides of (N, C, H, W); the W stride must be 1 (the caller makes rows
  *     contiguous).  NULL strides mean contiguous.
@@ -166,6 +167,26 @@ int sm_warp_by_flow(const void* image, const void* flow, void* out, int dtype,
                     int64_t N, int64_t C, int64_t Hi, int64_t Wi, int64_t H, int64_t W,
                     int64_t flow_channels, const int64_t* image_strides,
                     const int64_t* flow_strides, void* stream);
+
+/* §8f-2: MobileStereoNetV4's cost volume -- model/mobile_stereo_net_v4.py:443-461 with the
+ * stacks :317-335 (replaces the 48-iteration interweave -> conv3d -> volume11 loop).
+ * For every disparity i < D: interweave(L[..., i:], R[..., :-i]) as a depth-64 volume ->
+ * Conv3d(1->16, (8,3,3), stride (8,1,1)) -> Conv3d(16->32, (4,3,3), /4) -> Conv3d(32->16,
+ * (2,3,3), /2), each with its eval-mode BatchNorm folded in and ReLU, zero padding 1 at the
+ * crop's borders -> 1x1 conv 16->1 (+BN folded) + ReLU, at x >= i of out (N, D, H, W)
+ * (0 at x < i).  featL/featR: (N, 32, H, W) float32 (strides as above); out contiguous float32.
+ * Folded weights, float32 device pointers in PyTorch layouts: w1 (16,8,3,3) b1 (16),
+ * w2 (32,16,4,3,3) b2 (32), w3 (16,32,2,3,3) b3 (16), w4 (16) b4 (1).
+ * workspace: device scratch of at least sm_v4_volume_workspace_bytes(N, H, W) bytes (per-pixel
+ * layer-1 tables + packed MFMA weights); the library allocates nothing.
+ * Arithmetic: layer 1 fp32; layers 2-3 bf16 MFMA over hi/lo-split fp32 operands (3 products). */
+int64_t sm_v4_volume_workspace_bytes(int64_t N, int64_t H, int64_t W);
+int sm_v4_volume(const void* featL, const void* featR, void* out, int dtype,
+                 int64_t N, int64_t C, int64_t H, int64_t W, int64_t D,
+                 const int64_t* l_strides, const int64_t* r_strides,
+                 const float* w1, const float* b1, const float* w2, const float* b2,
+                 const float* w3, const float* b3, const float* w4, const float* b4,
+                 void* workspace, int64_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -23,6 +23,12 @@ int band_h2_fused_entry(const void* left, const void* right, void* out, float* d
                         int64_t N, int64_t C, int64_t H, int64_t W, int64_t D,
                         const int64_t* l_strides, const int64_t* r_strides, int mode,
                         void* stream, bool* handled);
+size_t v4_workspace_bytes(int64_t N, int64_t H, int64_t W);
+int v4_volume_entry(const float* L, const float* R, float* out, int64_t N, int64_t C, int64_t H,
+                    int64_t W, int64_t D, const int64_t* l_strides, const int64_t* r_strides,
+                    const float* w1, const float* b1, const float* w2, const float* b2,
+                    const float* w3, const float* b3, const float* w4, const float* b4,
+                    void* workspace, size_t workspace_bytes, hipStream_t st);
 int band_ws_entry(const void* left, const void* right, void* out, int dtype, int64_t N, int64_t C,
                   int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
                   const int64_t* r_strides, int mode, void* stream, bool* handled);
@@ -219,4 +225,23 @@ extern "C" int sm_warp_by_flow(const void* image, const void* flow, void* out, i
   SM_ENTRY_BEGIN
   return warp_entry(image, flow, out, dtype, N, C, Hi, Wi, H, W, flow_channels, image_strides,
                     flow_strides, stream);
+}
+
+extern "C" int64_t sm_v4_volume_workspace_bytes(int64_t N, int64_t H, int64_t W) {
+  if (N < 0 || H < 0 || W < 0) return -1;
+  return (int64_t)v4_workspace_bytes(N, H, W);
+}
+
+extern "C" int sm_v4_volume(const void* featL, const void* featR, void* out, int dtype, int64_t N,
+                            int64_t C, int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
+                            const int64_t* r_strides, const float* w1, const float* b1,
+                            const float* w2, const float* b2, const float* w3, const float* b3,
+                            const float* w4, const float* b4, void* workspace,
+                            int64_t workspace_bytes, void* stream) {
+  SM_ENTRY_BEGIN
+  if (dtype != SM_F32) return fail(SM_EDTYPE, "v4_volume: float32 features only");
+  if (workspace_bytes < 0) return fail(SM_EINVAL, "v4_volume: negative workspace size");
+  return v4_volume_entry(static_cast<const float*>(featL), static_cast<const float*>(featR),
+                         static_cast<float*>(out), N, C, H, W, D, l_strides, r_strides, w1, b1, w2,
+                         b2, w3, b3, w4, b4, workspace, (size_t)workspace_bytes, as_stream(stream));
 }

@@ -1,0 +1,465 @@
+// MobileStereoNetV4's interweave + Conv3d cost volume on gfx950.
+//
+// Reference (model/mobile_stereo_net_v4.py:443-461, stacks :317-335): for every disparity
+// i < D, X = interweave(L[..., i:], R[..., :-i]) -- even channels L, odd channels R -- is read as
+// a depth-64 volume of width W - i; Conv3d(1->16, (8,3,3), stride 8), (16->32, (4,3,3), stride 4),
+// (32->16, (2,3,3), stride 2), each + BatchNorm + ReLU, zero padding 1 at the CROP's borders;
+// then a 1x1 conv 16->1 + BatchNorm + ReLU; the result lands at x >= i of a zero (N, D, H, W)
+// volume.  Eval-mode BatchNorm is folded into the weights by the caller.
+//
+// Decomposition.  Stride == kernel depth, so the depth axis is block-diagonal:
+//   a1[b][o1](y,x)  = relu(b1 + PL[b][o1](y,x) + PR[b][o1](y,x-i))     b = depth block 0..7
+//   a2[b2][o2](y,x) = relu(b2 + sum_{kd<4, o1, 3x3} W2 a1[4 b2 + kd][o1])  b2 = 0, 1
+//   a3[o3](y,x)     = relu(b3 + sum_{b2, o2, 3x3} W3 a2[b2][o2])
+//   out(y,x)        = relu(b4 + sum_{o3} w4 a3[o3])
+// Layer 1 is linear before its ReLU and every one of its input channels is either L or R, so it
+// splits into a left part PL(y,x) and a right part PR(y,x-i) that do NOT depend on i: the
+// "tables" kernel computes them once per pixel (fp32 FMA), plus the single-column pieces that
+// the crop removes (dx = -1 of L at x = i, dx = +1 of R at x = W - 1).  Layers 2 and 3 (92 k of
+// the ~110 k flops per cell) run on v_mfma_f32_32x32x16_bf16 / 16x16x32_bf16 with every fp32
+// operand split into bf16 hi + lo and three products (hh + hl + lh; |error| <= ~2^-16 relative per
+// product, fp32 accumulation).
+//
+// Main kernel.  A workgroup owns (n, i, a 30-pixel column strip, a band of rows) and streams down
+// the rows with three-row LDS rings of a1 (34 px halo, 8 x 16 channels) and a2 (34 px, 64
+// channels).  Each of the 8 waves keeps ITS weights in VGPRs for the whole kernel: wave b holds
+// the layer-2 fragments of depth block b (9 taps x 16 x 32, kd = b & 3) and a quarter of the
+// layer-3 K range of one 16-pixel half; partial sums meet in LDS.  Per row: a1 row (tables ->
+// relu -> split, prefetched one row ahead) | layer 2 | reduce + bias + relu -> a2 row | layer 3 |
+// reduce + bias + relu + 1x1 + relu -> output row.
+#include "common.h"
+
+#include <atomic>
+
+namespace smcv {
+namespace v4vol {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+constexpr int kC = 32;       // feature channels per side (V4's preconv11 output)
+constexpr int kCh = 128;     // layer-1 channels: 8 depth blocks x 16
+constexpr int kTX = 30;      // output pixels per strip
+constexpr int kA2 = 34;      // a2 ring pixels (32 computed: x0-1 .. x0+30, +2 readable pad)
+constexpr int kA1 = 34;      // a1 ring pixels: x0-2 .. x0+31
+constexpr int kThreads = 512;
+
+// LDS layout (bytes)
+constexpr int kA1Slot = 8 * kA1 * 16 * 2;      // one row: [b 8][p 34][16 ch] bf16
+constexpr int kA1Plane = 3 * kA1Slot;          // three rows
+constexpr int kA2Slot = kA2 * 64 * 2;          // one row: [p 34][64 ch] bf16
+constexpr int kA2Plane = 3 * kA2Slot;
+constexpr int kOffA1 = 0;                                  // hi plane, then lo plane
+constexpr int kOffA2 = kOffA1 + 2 * kA1Plane;
+constexpr int kOffP2 = kOffA2 + 2 * kA2Plane;              // [8 waves][32 px][32 o2] fp32
+constexpr int kOffP3 = kOffP2 + 8 * 32 * 32 * 4;           // [8 waves][16 px][16 o3] fp32
+constexpr int kShm = kOffP3 + 8 * 16 * 16 * 4;
+static_assert(kShm <= 160 * 1024, "one workgroup per CU");
+
+// layer-3 K steps (18 = 9 taps x 2 halves of 64 a2 channels) per K group of 4
+__device__ __forceinline__ int ks_begin(int g) { return g == 0 ? 0 : g == 1 ? 5 : g == 2 ? 10 : 14; }
+__device__ __forceinline__ int ks_end(int g) { return g == 0 ? 5 : g == 1 ? 10 : g == 2 ? 14 : 18; }
+
+struct Args {
+  const float* T;        // tables [n][y][x][4][128]: PL, PLm (dx=-1 of L), PR, PRp (dx=+1 of R)
+  const bf16x8* P2;      // layer-2 B fragments [kd 4][tap 9][lane 64] hi, then the same lo
+  const bf16x8* P3;      // layer-3 B fragments [step 18][lane 64] hi, then lo
+  const float* b1;       // (16)
+  const float* b2;       // (32)
+  const float* b3;       // (16)
+  const float* w4;       // (16)
+  const float* b4;       // (1)
+  float* out;            // (N, D, H, W) contiguous
+  int N, H, W, D, strips, bands, BH;
+};
+
+__device__ __forceinline__ void split8(const float (&v)[8], bf16x8& hi, bf16x8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 h = (__bf16)v[j];
+    hi[j] = h;
+    lo[j] = (__bf16)(v[j] - (float)h);
+  }
+}
+
+// ------------------------------------------------------------------------------ tables
+// One thread per (pixel, layer-1 channel c = 16 b + o1): the left / right halves of layer 1
+// (3x3, zero padding at the image borders) and the two crop-border pieces.
+__global__ __launch_bounds__(256) void v4_tables(const float* __restrict__ L,
+                                                 const float* __restrict__ R, Strides4 ls,
+                                                 Strides4 rs, const float* __restrict__ w1,
+                                                 float* __restrict__ T, int N, int H, int W) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t npx = (int64_t)N * H * W;
+  if (t >= npx * kCh) return;
+  const int c = (int)(t & (kCh - 1));
+  const int64_t px = t >> 7;
+  const int x = (int)(px % W);
+  const int y = (int)((px / W) % H);
+  const int n = (int)(px / ((int64_t)W * H));
+  const int b = c >> 4, o1 = c & 15;
+  float pl = 0.f, plm = 0.f, pr = 0.f, prp = 0.f;
+  for (int kk = 0; kk < 4; ++kk) {
+    const int ch = 4 * b + kk;
+    const float* lp = L + n * ls.n + (int64_t)ch * ls.c;
+    const float* rp = R + n * rs.n + (int64_t)ch * rs.c;
+    for (int dy = 0; dy < 3; ++dy) {
+      const int yy = y + dy - 1;
+      if (yy < 0 || yy >= H) continue;
+      for (int dx = 0; dx < 3; ++dx) {
+        const int xx = x + dx - 1;
+        if (xx < 0 || xx >= W) continue;
+        const float wl = w1[((o1 * 8 + 2 * kk) * 3 + dy) * 3 + dx];
+        const float wr = w1[((o1 * 8 + 2 * kk + 1) * 3 + dy) * 3 + dx];
+        const float lv = lp[(int64_t)yy * ls.h + xx] * wl;
+        const float rv = rp[(int64_t)yy * rs.h + xx] * wr;
+        pl += lv;
+        pr += rv;
+        if (dx == 0) plm += lv;
+        if (dx == 2) prp += rv;
+      }
+    }
+  }
+  float* o = T + px * (4 * kCh) + c;
+  o[0] = pl;
+  o[kCh] = plm;
+  o[2 * kCh] = pr;
+  o[3 * kCh] = prp;
+}
+
+// ------------------------------------------------------------------------------ weight packing
+// The MFMA B fragments, split into bf16 hi / lo.  Layer 2 (32x32x16): lane l holds
+// B[k = 8 (l>>5) + j][col l&31] = W2[o2 = l&31][o1 = 8 (l>>5) + j][kd][dy][dx].  Layer 3
+// (16x16x32): step s = 2 tap + half, lane l holds B[k = 8 (l>>4) + j][col l&15] =
+// W3[o3 = l&15][o2 = k][kd = half][dy][dx].
+__global__ __launch_bounds__(256) void v4_pack(const float* __restrict__ w2,
+                                               const float* __restrict__ w3,
+                                               __bf16* __restrict__ P2, __bf16* __restrict__ P3) {
+  constexpr int n2 = 4 * 9 * 64 * 8, n3 = 18 * 64 * 8;
+  for (int e = threadIdx.x + blockIdx.x * 256; e < n2 + n3; e += 256 * gridDim.x) {
+    float v;
+    __bf16* hp;
+    int off, total;
+    if (e < n2) {
+      const int j = e & 7, lane = (e >> 3) & 63, tap = (e >> 9) % 9, kd = (e >> 9) / 9;
+      const int o2 = lane & 31, o1 = 8 * (lane >> 5) + j;
+      v = w2[(((o2 * 16 + o1) * 4 + kd) * 3 + tap / 3) * 3 + tap % 3];
+      hp = P2;
+      off = e;
+      total = n2;
+    } else {
+      const int f = e - n2;
+      const int j = f & 7, lane = (f >> 3) & 63, s = f >> 9;
+      const int tap = s >> 1, half = s & 1;
+      const int o3 = lane & 15, o2 = 8 * (lane >> 4) + j;
+      v = w3[(((o3 * 32 + o2) * 2 + half) * 3 + tap / 3) * 3 + tap % 3];
+      hp = P3;
+      off = f;
+      total = n3;
+    }
+    const __bf16 h = (__bf16)v;
+    hp[off] = h;
+    hp[total + off] = (__bf16)(v - (float)h);
+  }
+}
+
+// ------------------------------------------------------------------------------ main kernel
+__global__ __launch_bounds__(kThreads, 1) void v4_main(Args a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // work: (n, i, strip, band), the band fastest so a CU's neighbours share table rows in L2
+  int w = blockIdx.x;
+  const int band = w % a.bands;
+  w /= a.bands;
+  const int strip = w % a.strips;
+  w /= a.strips;
+  const int i = w % a.D;
+  const int n = w / a.D;
+  const int H = a.H, W = a.W;
+  const int x0 = strip * kTX;
+  const int y0 = band * a.BH, y1 = min(H, y0 + a.BH);
+  float* outp = a.out + ((int64_t)n * a.D + i) * H * W;
+  if (x0 + kTX <= i || i >= W) {  // every output of the strip lies at x < i: zeros
+    for (int e = tid; e < (y1 - y0) * kTX; e += kThreads) {
+      const int r = y0 + e / kTX, x = x0 + e % kTX;
+      if (x < W) outp[(int64_t)r * W + x] = 0.f;
+    }
+    return;
+  }
+
+  // ---- resident weights
+  bf16x8 w2h[9], w2l[9];
+  {
+    const int kd = wave & 3;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      w2h[t] = a.P2[(kd * 9 + t) * 64 + lane];
+      w2l[t] = a.P2[4 * 9 * 64 + (kd * 9 + t) * 64 + lane];
+    }
+  }
+  const int mb = wave & 1, kg = wave >> 1;  // layer 3: 16-pixel half, K group
+  const int s0 = ks_begin(kg), s1 = ks_end(kg);
+  bf16x8 w3h[5], w3l[5];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    const int s = min(s0 + q, 17);
+    w3h[q] = a.P3[s * 64 + lane];
+    w3l[q] = a.P3[18 * 64 + s * 64 + lane];
+  }
+
+  unsigned char* a1h = smem + kOffA1;
+  unsigned char* a1l = a1h + kA1Plane;
+  unsigned char* a2h = smem + kOffA2;
+  unsigned char* a2l = a2h + kA2Plane;
+  float* part2 = reinterpret_cast<float*>(smem + kOffP2);
+  float* part3 = reinterpret_cast<float*>(smem + kOffP3);
+
+  // ---- a1 row prefetch: lane task = (pixel p, channel half hh) of wave b = `wave`; 68 tasks
+  struct Pre {
+    f32x4v pl[2][2], pr[2][2], fix[2][2];
+  };
+  auto fetch = [&](int s, Pre& pf) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int task = lane + 64 * u;
+      const int p = task >> 1, hh = task & 1;
+      const int x = x0 - 2 + p;
+      const bool ok = task < 2 * kA1 && s >= 0 && s < H && x >= i && x < W;
+      const int c = wave * 16 + hh * 8;
+      f32x4v z = {0.f, 0.f, 0.f, 0.f};
+      pf.pl[u][0] = pf.pl[u][1] = pf.pr[u][0] = pf.pr[u][1] = pf.fix[u][0] = pf.fix[u][1] = z;
+      if (ok) {
+        const float* tl = a.T + (((int64_t)n * H + s) * W + x) * (4 * kCh) + c;
+        const float* tr = a.T + (((int64_t)n * H + s) * W + (x - i)) * (4 * kCh) + 2 * kCh + c;
+        pf.pl[u][0] = *reinterpret_cast<const f32x4v*>(tl);
+        pf.pl[u][1] = *reinterpret_cast<const f32x4v*>(tl + 4);
+        pf.pr[u][0] = *reinterpret_cast<const f32x4v*>(tr);
+        pf.pr[u][1] = *reinterpret_cast<const f32x4v*>(tr + 4);
+        // the crop's borders: no L at x - 1 when x == i, no R at x + 1 when x == W - 1
+        if (x == i) {
+          f32x4v m0 = *reinterpret_cast<const f32x4v*>(tl + kCh);
+          f32x4v m1 = *reinterpret_cast<const f32x4v*>(tl + kCh + 4);
+          pf.fix[u][0] += m0;
+          pf.fix[u][1] += m1;
+        }
+        if (x == W - 1) {
+          f32x4v m0 = *reinterpret_cast<const f32x4v*>(tr + kCh);
+          f32x4v m1 = *reinterpret_cast<const f32x4v*>(tr + kCh + 4);
+          pf.fix[u][0] += m0;
+          pf.fix[u][1] += m1;
+        }
+      }
+    }
+  };
+  float bias1[8][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bias1[j][u] = a.b1[(((lane + 64 * u) & 1) * 8) + j];
+  // a1 = relu(b1 + PL - fix + PR) for valid cells, 0 elsewhere (the crop's zero padding)
+  auto put_a1 = [&](int s, const Pre& pf) {
+    const int slot = ((s % 3) + 3) % 3;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int task = lane + 64 * u;
+      if (task >= 2 * kA1) continue;
+      const int p = task >> 1, hh = task & 1;
+      const int x = x0 - 2 + p;
+      const bool ok = s >= 0 && s < H && x >= i && x < W;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float pl = pf.pl[u][j >> 2][j & 3], pr = pf.pr[u][j >> 2][j & 3];
+        const float fx = pf.fix[u][j >> 2][j & 3];
+        v[j] = ok ? fmaxf(bias1[j][u] + ((pl - fx) + pr), 0.f) : 0.f;
+      }
+      bf16x8 h, l;
+      split8(v, h, l);
+      const int off = slot * kA1Slot + ((wave * kA1 + p) * 16 + hh * 8) * 2;
+      *reinterpret_cast<bf16x8*>(a1h + off) = h;
+      *reinterpret_cast<bf16x8*>(a1l + off) = l;
+    }
+  };
+
+  Pre pf;
+  fetch(y0 - 2, pf);
+  for (int s = y0 - 2; s <= y1 + 1; ++s) {
+    // ---- a1 row s
+    put_a1(s, pf);
+    if (s + 1 <= y1 + 1) fetch(s + 1, pf);
+    __syncthreads();
+    const int q = s - 1;  // a2 row
+    if (s >= y0) {
+      // ---- layer 2, depth block `wave`: 9 taps x 3 products, K = 16 channels each
+      f32x16 acc = {};
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int dy = t / 3, dx = t % 3;
+        const int slot = ((q + dy - 1) % 3 + 3) % 3;
+        const int m = lane & 31, h = lane >> 5;
+        const int off = slot * kA1Slot + ((wave * kA1 + m + dx) * 16 + 8 * h) * 2;
+        const bf16x8 ah = *reinterpret_cast<const bf16x8*>(a1h + off);
+        const bf16x8 al = *reinterpret_cast<const bf16x8*>(a1l + off);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, w2h[t], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, w2l[t], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, w2h[t], acc, 0, 0, 0);
+      }
+      // partial [wave][px][o2]: lane holds col o2 = lane & 31, rows (r&3) + 8 (r>>2) + 4 (lane>>5)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        part2[(wave * 32 + m) * 32 + (lane & 31)] = acc[r];
+      }
+    }
+    __syncthreads();
+    if (s >= y0) {
+      // ---- a2 row q = relu(b2 + sum of the 4 depth blocks of its half), masked
+      const int m = tid >> 4, g = tid & 15;  // pixel, group of 4 channels (ch = 32 b2 + o2)
+      const int b2 = g >> 3, o2 = (4 * g) & 31;
+      const int x = x0 - 1 + m;
+      const bool ok = q >= 0 && q < H && x >= i && x < W;
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = a.b2[o2 + j];
+#pragma unroll
+      for (int kd = 0; kd < 4; ++kd) {
+        const f32x4v pv = *reinterpret_cast<const f32x4v*>(part2 + ((4 * b2 + kd) * 32 + m) * 32 + o2);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] += pv[j];
+      }
+      bf16x4 h, l;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float vv = ok ? fmaxf(v[j], 0.f) : 0.f;
+        const __bf16 hb = (__bf16)vv;
+        h[j] = hb;
+        l[j] = (__bf16)(vv - (float)hb);
+      }
+      const int slot = ((q % 3) + 3) % 3;
+      const int off = slot * kA2Slot + (m * 64 + 4 * g) * 2;
+      *reinterpret_cast<bf16x4*>(a2h + off) = h;
+      *reinterpret_cast<bf16x4*>(a2l + off) = l;
+      if (m < 2) {  // the ring's 2 readable pad pixels (32, 33): zeros
+        const int off2 = slot * kA2Slot + ((32 + m) * 64 + 4 * g) * 2;
+        const bf16x4 z = {};
+        *reinterpret_cast<bf16x4*>(a2h + off2) = z;
+        *reinterpret_cast<bf16x4*>(a2l + off2) = z;
+      }
+    }
+    __syncthreads();
+    const int r = s - 2;  // output row
+    if (s >= y0 + 2) {
+      // ---- layer 3: this wave's K steps for its 16-pixel half
+      f32x4v acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int qq = 0; qq < 5; ++qq) {
+        const int st = s0 + qq;
+        if (st < s1) {
+          const int tap = st >> 1, half = st & 1, dy = tap / 3, dx = tap % 3;
+          const int slot = ((r + dy - 1) % 3 + 3) % 3;
+          const int px = 16 * mb + (lane & 15) + dx;
+          const int off = slot * kA2Slot + (px * 64 + half * 32 + 8 * (lane >> 4)) * 2;
+          const bf16x8 ah = *reinterpret_cast<const bf16x8*>(a2h + off);
+          const bf16x8 al = *reinterpret_cast<const bf16x8*>(a2l + off);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, w3h[qq], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, w3l[qq], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, w3h[qq], acc, 0, 0, 0);
+        }
+      }
+      // partial [wave][px 16][o3 16]: col o3 = lane & 15, rows (lane >> 4) * 4 + reg
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        part3[(wave * 16 + (lane >> 4) * 4 + rr) * 16 + (lane & 15)] = acc[rr];
+    }
+    __syncthreads();
+    if (s >= y0 + 2 && tid < 512) {
+      // ---- a3 = relu(b3 + sum over the 4 K groups), out = relu(b4 + w4 . a3), masked
+      const int o = tid >> 4, o3 = tid & 15;  // output pixel 0..31, channel
+      const int half = o >> 4, ol = o & 15;
+      float v = a.b3[o3];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) v += part3[((2 * g + half) * 16 + ol) * 16 + o3];
+      v = fmaxf(v, 0.f) * a.w4[o3];
+      // sum over the 16 lanes of this pixel (aligned 16-lane groups of the wave)
+#pragma unroll
+      for (int sh = 8; sh >= 1; sh >>= 1) v += __shfl_xor(v, sh, 16);
+      const int x = x0 + o;
+      if (o3 == 0 && o < kTX && x < W) outp[(int64_t)r * W + x] = x >= i ? fmaxf(v + a.b4[0], 0.f) : 0.f;
+    }
+  }
+}
+
+}  // namespace v4vol
+
+size_t v4_workspace_bytes(int64_t N, int64_t H, int64_t W) {
+  const size_t tables = (size_t)N * H * W * 4 * v4vol::kCh * sizeof(float);
+  const size_t packed = (size_t)2 * (4 * 9 * 64 * 8 + 18 * 64 * 8) * 2;
+  return ((tables + 255) / 256) * 256 + packed;
+}
+
+int v4_volume_entry(const float* L, const float* R, float* out, int64_t N, int64_t C, int64_t H,
+                    int64_t W, int64_t D, const int64_t* l_strides, const int64_t* r_strides,
+                    const float* w1, const float* b1, const float* w2, const float* b2,
+                    const float* w3, const float* b3, const float* w4, const float* b4,
+                    void* workspace, size_t workspace_bytes, hipStream_t st) {
+  using namespace v4vol;
+  if (N < 0 || H < 0 || W < 0 || D < 0) return fail(SM_EINVAL, "v4_volume: negative size");
+  if (C != kC) return fail(SM_EUNSUPPORTED, "v4_volume: the V4 stack needs C = 32 feature channels");
+  if (N * D * H * W == 0) return SM_OK;
+  if (!L || !R || !out || !w1 || !b1 || !w2 || !b2 || !w3 || !b3 || !w4 || !b4 || !workspace)
+    return fail(SM_EINVAL, "v4_volume: null pointer");
+  if (workspace_bytes < v4_workspace_bytes(N, H, W))
+    return fail(SM_EINVAL, "v4_volume: workspace too small (sm_v4_volume_workspace_bytes)");
+  if (H * W >= ((int64_t)1 << 31) / (4 * kCh) / std::max<int64_t>(N, 1) || W >= (1 << 24))
+    return fail(SM_EINVAL, "v4_volume: planes too large");
+  Strides4 ls, rs;
+  int rc = read_strides(l_strides, C, H, W, &ls, "left");
+  if (rc != SM_OK) return rc;
+  rc = read_strides(r_strides, C, H, W, &rs, "right");
+  if (rc != SM_OK) return rc;
+  float* T = static_cast<float*>(workspace);
+  const size_t tables = (size_t)N * H * W * 4 * kCh * sizeof(float);
+  __bf16* P2 = reinterpret_cast<__bf16*>(static_cast<unsigned char*>(workspace) + ((tables + 255) / 256) * 256);
+  __bf16* P3 = P2 + 2 * (4 * 9 * 64 * 8);
+  const int64_t nthreads = N * H * W * kCh;
+  hipLaunchKernelGGL(v4_tables, dim3((unsigned)ceil_div(nthreads, 256)), dim3(256), 0, st, L, R, ls,
+                     rs, w1, T, (int)N, (int)H, (int)W);
+  rc = check_launch("v4_tables");
+  if (rc != SM_OK) return rc;
+  hipLaunchKernelGGL(v4_pack, dim3(16), dim3(256), 0, st, w2, w3, P2, P3);
+  rc = check_launch("v4_pack");
+  if (rc != SM_OK) return rc;
+  Args a;
+  a.T = T;
+  a.P2 = reinterpret_cast<const bf16x8*>(P2);
+  a.P3 = reinterpret_cast<const bf16x8*>(P3);
+  a.b1 = b1;
+  a.b2 = b2;
+  a.b3 = b3;
+  a.w4 = w4;
+  a.b4 = b4;
+  a.out = out;
+  a.N = (int)N;
+  a.H = (int)H;
+  a.W = (int)W;
+  a.D = (int)D;
+  a.strips = (int)ceil_div(W, kTX);
+  // row bands: enough workgroups to fill the chip twice, at most ~8 % halo rows
+  const int64_t base = N * D * a.strips;
+  int bands = (int)std::min<int64_t>(std::max<int64_t>(1, ceil_div(2048, std::max<int64_t>(base, 1))),
+                                     std::max<int64_t>(1, H / 24));
+  a.BH = (int)ceil_div(H, bands);
+  a.bands = (int)ceil_div(H, a.BH);
+  const int64_t nwg = base * a.bands;
+  if (nwg >= INT32_MAX) return fail(SM_EINVAL, "v4_volume: too much work for one launch");
+  static std::atomic<unsigned long long> lds_done{0};
+  const int dev = stream_device(st);
+  rc = ensure_lds_limit(reinterpret_cast<const void*>(v4_main), kShm, dev, lds_done);
+  if (rc != SM_OK) return rc;
+  hipLaunchKernelGGL(v4_main, dim3((unsigned)nwg), dim3(kThreads), kShm, st, a);
+  return check_launch("v4_main");
+}
+
+}  // namespace smcv

@@ -21,6 +21,7 @@ Reference operators mirrored (babiking/realtime_stereo_matcher):
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -275,6 +276,37 @@ def interweave_volume(left, right, max_disparity):
                 _ptr(left), _ptr(right), _ptr(out), code, n, c, h, w, D,
                 _lib.strides_arg(left), _lib.strides_arg(right), _stream(dev)),
                 "sm_cv_interweave_shifted")
+        return out
+
+    return _run(fn, left, right)
+
+
+def v4_volume(featL, featR, w1, b1, w2, b2, w3, b3, w4, b4, volume_size=48):
+    """MobileStereoNetV4's cost volume (model/mobile_stereo_net_v4.py:443-461):
+    (N,32,H,W) fp32 x2 -> (N,D,H,W) fp32, slice i = volume11(conv3d(interweave(L[..., i:],
+    R[..., :-i]))) at x >= i, 0 elsewhere, from eval-mode-folded weights
+    (``model.mobile_stereo_net_v4.fold_v4_weights``)."""
+    left, right, dev, code = _pair(featL, featR, "v4_volume")
+    if code != _lib.SM_F32:
+        raise TypeError("v4_volume: float32 features only")
+    D = _disp(volume_size, "v4_volume")
+    n, c, h, w = left.shape
+    ws = [t.detach().to(device=dev, dtype=torch.float32).contiguous() for t in (w1, b1, w2, b2, w3, b3, w4, b4)]
+    shapes = [(16, 8, 3, 3), (16,), (32, 16, 4, 3, 3), (32,), (16, 32, 2, 3, 3), (16,), (16,), (1,)]
+    for t, shp in zip(ws, shapes):
+        if t.numel() != int(np.prod(shp)):
+            raise ValueError(f"v4_volume: weight of {t.numel()} elements, expected shape {shp}")
+
+    def fn():
+        out = torch.empty((n, D, h, w), dtype=torch.float32, device=dev)
+        if out.numel():
+            lib = _lib.load()
+            nbytes = int(lib.sm_v4_volume_workspace_bytes(n, h, w))
+            scratch = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            _lib.check(lib.sm_v4_volume(
+                _ptr(left), _ptr(right), _ptr(out), code, n, c, h, w, D,
+                _lib.strides_arg(left), _lib.strides_arg(right), *[_ptr(t) for t in ws],
+                _ptr(scratch), nbytes, _stream(dev)), "sm_v4_volume")
         return out
 
     return _run(fn, left, right)

@@ -15,7 +15,7 @@ HEADER = os.path.join(ROOT, "include", "stereocv.h")
 
 def declared_symbols():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:const char\*|int)\s+(sm_[a-z0-9_]+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:const char\*|int64_t|int)\s+(sm_[a-z0-9_]+)\s*\(", src, re.M)))
 
 
 def test_header_declares_the_abi():

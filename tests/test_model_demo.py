@@ -15,9 +15,11 @@ NETS = {"v1": ("MobileStereoNetHIP", {}),
                                       "refine_dim": 7, "refine_dilates": (1, 2, 4, 8, 1, 1)}),
         "v3": ("MobileStereoNetV3HIP", {"down_factor": 3, "max_disp": 192,
                                         "refine_dilates": (1, 2, 4, 8, 1, 1), "hidden_dim": 32}),
-        "dispnetc": ("MobileDispNetCHIP", {"hidden_dim": 8, "max_disp": 192, "with_batch_norm": True})}
+        "dispnetc": ("MobileDispNetCHIP", {"hidden_dim": 8, "max_disp": 192, "with_batch_norm": True}),
+        "v4": ("MobileStereoNetV4HIP", {"max_disp": 192})}  # stereo_net_config_v4.json
 FILES = {"v1": "model_msn_v1.npz", "v2": "model_msn_v2.npz", "v3": "model_msn_v3.npz",
-         "dispnetc": "model_dispnetc.npz"}
+         "dispnetc": "model_dispnetc.npz", "v4": "model_msn_v4.npz"}
+NOUT = {"v1": 3, "v2": 3, "v3": 3, "dispnetc": 6, "v4": 1}
 
 
 def _fixture(v):
@@ -25,10 +27,10 @@ def _fixture(v):
 
 
 def _net(a, v):
-    from realtime_stereo_matcher_amd.model import stereo_nets
+    from realtime_stereo_matcher_amd.model import stereo_net_v4, stereo_nets
 
     cls, kw = NETS[v]
-    net = getattr(stereo_nets, cls)(**kw)
+    net = getattr(stereo_net_v4 if v == "v4" else stereo_nets, cls)(**kw)
     if "weight_seed" in a.files:  # synthetic weights regenerated from the recorded seed
         from model_weights import seeded_state
 
@@ -57,7 +59,7 @@ def test_model_outputs_match_reference(v):
     net = _net(a, v).cuda()
     with torch.no_grad():
         outs = net(torch.from_numpy(a["left"]).cuda(), torch.from_numpy(a["right"]).cuda())
-    assert len(outs) == (6 if v == "dispnetc" else 3)
+    assert len(outs) == NOUT[v]
     for i, o in enumerate(outs):
         ref = a[f"out{i}"]
         assert tuple(o.shape) == ref.shape

@@ -1,5 +1,7 @@
 """Pin the CPU oracle (oracle/stereo_oracle.py) and the eager CPU port (oracle/torch_port.py)
 against the golden vectors recorded from the reference's own modules (CPU-only tests)."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -7,6 +9,8 @@ import torch
 from conftest import cases, load_case
 from oracle import stereo_oracle as O
 from oracle import torch_port as P
+
+GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 TOL_F32 = 1e-4  # north-star fp32 bar (BASELINE.json)
 
@@ -188,3 +192,21 @@ def test_model_weights_deterministic():
     assert all(torch.equal(s1[k], s2[k]) for k in layout)
     assert not torch.equal(seeded_state(layout, 6)["a.weight"], s1["a.weight"])
     assert float(s1["bn.running_var"].min()) >= 0.75
+
+
+V4_FILES = sorted(f for f in os.listdir(GOLDEN_DIR) if f.startswith("v4_volume_"))
+
+
+def v4_case(name):
+    """A §8f-2 fixture: inputs, the conv3d / volume11 parameters (``p/`` keys) and the volume
+    the reference loop produced (tests/golden/gen_model_golden.py)."""
+    a = np.load(os.path.join(GOLDEN_DIR, name))  # allow_pickle=False: data only
+    return a, {k[2:]: a[k] for k in a.files if k.startswith("p/")}
+
+
+@pytest.mark.parametrize("name", V4_FILES)
+def test_v4_volume(name):
+    """The V4 interweave + Conv3d cost-volume restatement (model/mobile_stereo_net_v4.py:443-461)
+    against the reference loop's own output."""
+    a, p = v4_case(name)
+    np.testing.assert_allclose(O.v4_volume(a["featL"], a["featR"], p, 48), a["volume"], atol=1e-5, rtol=0)
