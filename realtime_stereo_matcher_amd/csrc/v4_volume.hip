@@ -41,9 +41,9 @@ typedef float f32x4v __attribute__((ext_vector_type(4)));
 
 constexpr int kC = 32;       // feature channels per side (V4's preconv11 output)
 constexpr int kCh = 128;     // layer-1 channels: 8 depth blocks x 16
-constexpr int kTX = 30;      // output pixels per strip
-constexpr int kA2 = 34;      // a2 ring pixels (32 computed: x0-1 .. x0+30, +2 readable pad)
-constexpr int kA1 = 34;      // a1 ring pixels: x0-2 .. x0+31
+constexpr int kTX = 28;      // output pixels per strip
+constexpr int kA2 = 34;      // a2 ring pixels: 32 computed (x0-1 .. x0+30; 30 used) + 2 readable pad
+constexpr int kA1 = 34;      // a1 ring pixels: 32 computed (x0-2 .. x0+29) + 2 zero pad
 constexpr int kThreads = 512;
 
 // LDS layout (bytes)
@@ -63,7 +63,7 @@ __device__ __forceinline__ int ks_begin(int g) { return g == 0 ? 0 : g == 1 ? 5 
 __device__ __forceinline__ int ks_end(int g) { return g == 0 ? 5 : g == 1 ? 10 : g == 2 ? 14 : 18; }
 
 struct Args {
-  const float* T;        // tables [n][y][x][4][128]: PL, PLm (dx=-1 of L), PR, PRp (dx=+1 of R)
+  const float* T;        // tables [n][y][x][4][128]: PL, PL without dx=-1, PR, PR without dx=+1
   const bf16x8* P2;      // layer-2 B fragments [kd 4][tap 9][lane 64] hi, then the same lo
   const bf16x8* P3;      // layer-3 B fragments [step 18][lane 64] hi, then lo
   const float* b1;       // (16)
@@ -75,6 +75,13 @@ struct Args {
   int N, H, W, D, strips, bands, BH;
 };
 
+// Workgroup barrier for LDS hand-offs only: this wave's LDS accesses are complete, then
+// s_barrier.  The prefetched table loads and the output stores stay in flight (__syncthreads()
+// would drain them with vmcnt(0) at every one of the four barriers of a row).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 __device__ __forceinline__ void split8(const float (&v)[8], bf16x8& hi, bf16x8& lo) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -85,48 +92,57 @@ __device__ __forceinline__ void split8(const float (&v)[8], bf16x8& hi, bf16x8& 
 }
 
 // ------------------------------------------------------------------------------ tables
-// One thread per (pixel, layer-1 channel c = 16 b + o1): the left / right halves of layer 1
-// (3x3, zero padding at the image borders) and the two crop-border pieces.
+// One thread per (pixel, depth block b): the 16 layer-1 channels c = 16 b + o1 of the left and
+// right halves (3x3, zero padding at the image borders), each also without the column the crop
+// removes: L without its dx = -1 taps (used at x == i), R without its dx = +1 taps (used at
+// x == W - 1).  Adjacent threads take adjacent pixels (coalesced feature loads); w1 sits in LDS.
 __global__ __launch_bounds__(256) void v4_tables(const float* __restrict__ L,
                                                  const float* __restrict__ R, Strides4 ls,
                                                  Strides4 rs, const float* __restrict__ w1,
                                                  float* __restrict__ T, int N, int H, int W) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t npx = (int64_t)N * H * W;
-  if (t >= npx * kCh) return;
-  const int c = (int)(t & (kCh - 1));
-  const int64_t px = t >> 7;
+  __shared__ float ws[16 * 8 * 9];
+  for (int e = threadIdx.x; e < 16 * 8 * 9; e += 256) ws[e] = w1[e];
+  __syncthreads();
+  const int64_t px = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int b = blockIdx.y;
+  if (px >= (int64_t)N * H * W) return;
   const int x = (int)(px % W);
   const int y = (int)((px / W) % H);
   const int n = (int)(px / ((int64_t)W * H));
-  const int b = c >> 4, o1 = c & 15;
-  float pl = 0.f, plm = 0.f, pr = 0.f, prp = 0.f;
+  float lv[4][9], rv[4][9];
+#pragma unroll
   for (int kk = 0; kk < 4; ++kk) {
-    const int ch = 4 * b + kk;
-    const float* lp = L + n * ls.n + (int64_t)ch * ls.c;
-    const float* rp = R + n * rs.n + (int64_t)ch * rs.c;
-    for (int dy = 0; dy < 3; ++dy) {
-      const int yy = y + dy - 1;
-      if (yy < 0 || yy >= H) continue;
-      for (int dx = 0; dx < 3; ++dx) {
-        const int xx = x + dx - 1;
-        if (xx < 0 || xx >= W) continue;
-        const float wl = w1[((o1 * 8 + 2 * kk) * 3 + dy) * 3 + dx];
-        const float wr = w1[((o1 * 8 + 2 * kk + 1) * 3 + dy) * 3 + dx];
-        const float lv = lp[(int64_t)yy * ls.h + xx] * wl;
-        const float rv = rp[(int64_t)yy * rs.h + xx] * wr;
-        pl += lv;
-        pr += rv;
-        if (dx == 0) plm += lv;
-        if (dx == 2) prp += rv;
-      }
+    const float* lp = L + n * ls.n + (int64_t)(4 * b + kk) * ls.c;
+    const float* rp = R + n * rs.n + (int64_t)(4 * b + kk) * rs.c;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
+      const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
+      lv[kk][t] = ok ? lp[(int64_t)yy * ls.h + xx] : 0.f;
+      rv[kk][t] = ok ? rp[(int64_t)yy * rs.h + xx] : 0.f;
     }
   }
-  float* o = T + px * (4 * kCh) + c;
-  o[0] = pl;
-  o[kCh] = plm;
-  o[2 * kCh] = pr;
-  o[3 * kCh] = prp;
+  float* o = T + px * (4 * kCh) + 16 * b;
+#pragma unroll 4
+  for (int o1 = 0; o1 < 16; ++o1) {
+    float pl = 0.f, plm = 0.f, pr = 0.f, prp = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const float l = lv[kk][t] * ws[(o1 * 8 + 2 * kk) * 9 + t];
+        const float r = rv[kk][t] * ws[(o1 * 8 + 2 * kk + 1) * 9 + t];
+        pl += l;
+        pr += r;
+        if (t % 3 == 0) plm += l;
+        if (t % 3 == 2) prp += r;
+      }
+    }
+    o[o1] = pl;
+    o[kCh + o1] = pl - plm;
+    o[2 * kCh + o1] = pr;
+    o[3 * kCh + o1] = pr - prp;
+  }
 }
 
 // ------------------------------------------------------------------------------ weight packing
@@ -216,80 +232,59 @@ __global__ __launch_bounds__(kThreads, 1) void v4_main(Args a) {
   float* part2 = reinterpret_cast<float*>(smem + kOffP2);
   float* part3 = reinterpret_cast<float*>(smem + kOffP3);
 
-  // ---- a1 row prefetch: lane task = (pixel p, channel half hh) of wave b = `wave`; 68 tasks
+  // ---- a1 row prefetch: lane = (pixel p = lane >> 1, channel half hh) of depth block `wave`
   struct Pre {
-    f32x4v pl[2][2], pr[2][2], fix[2][2];
+    f32x4v pl[2], pr[2];
   };
+  const int pp = lane >> 1, hh = lane & 1;
+  const int xa = x0 - 2 + pp;   // this lane's a1 pixel
   auto fetch = [&](int s, Pre& pf) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int task = lane + 64 * u;
-      const int p = task >> 1, hh = task & 1;
-      const int x = x0 - 2 + p;
-      const bool ok = task < 2 * kA1 && s >= 0 && s < H && x >= i && x < W;
+    const bool ok = s >= 0 && s < H && xa >= i && xa < W;
+    const f32x4v z = {0.f, 0.f, 0.f, 0.f};
+    pf.pl[0] = pf.pl[1] = pf.pr[0] = pf.pr[1] = z;
+    if (ok) {
       const int c = wave * 16 + hh * 8;
-      f32x4v z = {0.f, 0.f, 0.f, 0.f};
-      pf.pl[u][0] = pf.pl[u][1] = pf.pr[u][0] = pf.pr[u][1] = pf.fix[u][0] = pf.fix[u][1] = z;
-      if (ok) {
-        const float* tl = a.T + (((int64_t)n * H + s) * W + x) * (4 * kCh) + c;
-        const float* tr = a.T + (((int64_t)n * H + s) * W + (x - i)) * (4 * kCh) + 2 * kCh + c;
-        pf.pl[u][0] = *reinterpret_cast<const f32x4v*>(tl);
-        pf.pl[u][1] = *reinterpret_cast<const f32x4v*>(tl + 4);
-        pf.pr[u][0] = *reinterpret_cast<const f32x4v*>(tr);
-        pf.pr[u][1] = *reinterpret_cast<const f32x4v*>(tr + 4);
-        // the crop's borders: no L at x - 1 when x == i, no R at x + 1 when x == W - 1
-        if (x == i) {
-          f32x4v m0 = *reinterpret_cast<const f32x4v*>(tl + kCh);
-          f32x4v m1 = *reinterpret_cast<const f32x4v*>(tl + kCh + 4);
-          pf.fix[u][0] += m0;
-          pf.fix[u][1] += m1;
-        }
-        if (x == W - 1) {
-          f32x4v m0 = *reinterpret_cast<const f32x4v*>(tr + kCh);
-          f32x4v m1 = *reinterpret_cast<const f32x4v*>(tr + kCh + 4);
-          pf.fix[u][0] += m0;
-          pf.fix[u][1] += m1;
-        }
-      }
+      // the crop's borders: no L at x - 1 when x == i, no R at x + 1 when x == W - 1
+      const float* tl = a.T + (((int64_t)n * H + s) * W + xa) * (4 * kCh) + (xa == i ? kCh : 0) + c;
+      const float* tr = a.T + (((int64_t)n * H + s) * W + (xa - i)) * (4 * kCh) +
+                        (xa == W - 1 ? 3 * kCh : 2 * kCh) + c;
+      pf.pl[0] = *reinterpret_cast<const f32x4v*>(tl);
+      pf.pl[1] = *reinterpret_cast<const f32x4v*>(tl + 4);
+      pf.pr[0] = *reinterpret_cast<const f32x4v*>(tr);
+      pf.pr[1] = *reinterpret_cast<const f32x4v*>(tr + 4);
     }
   };
-  float bias1[8][2];
+  float bias1[8];
 #pragma unroll
-  for (int u = 0; u < 2; ++u)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) bias1[j][u] = a.b1[(((lane + 64 * u) & 1) * 8) + j];
-  // a1 = relu(b1 + PL - fix + PR) for valid cells, 0 elsewhere (the crop's zero padding)
+  for (int j = 0; j < 8; ++j) bias1[j] = a.b1[hh * 8 + j];
+  // a1 = relu(b1 + PL + PR) for valid cells, 0 elsewhere (the crop's zero padding)
   auto put_a1 = [&](int s, const Pre& pf) {
     const int slot = ((s % 3) + 3) % 3;
+    const bool ok = s >= 0 && s < H && xa >= i && xa < W;
+    float v[8];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int task = lane + 64 * u;
-      if (task >= 2 * kA1) continue;
-      const int p = task >> 1, hh = task & 1;
-      const int x = x0 - 2 + p;
-      const bool ok = s >= 0 && s < H && x >= i && x < W;
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float pl = pf.pl[u][j >> 2][j & 3], pr = pf.pr[u][j >> 2][j & 3];
-        const float fx = pf.fix[u][j >> 2][j & 3];
-        v[j] = ok ? fmaxf(bias1[j][u] + ((pl - fx) + pr), 0.f) : 0.f;
-      }
-      bf16x8 h, l;
-      split8(v, h, l);
-      const int off = slot * kA1Slot + ((wave * kA1 + p) * 16 + hh * 8) * 2;
-      *reinterpret_cast<bf16x8*>(a1h + off) = h;
-      *reinterpret_cast<bf16x8*>(a1l + off) = l;
-    }
+    for (int j = 0; j < 8; ++j)
+      v[j] = ok ? fmaxf(bias1[j] + (pf.pl[j >> 2][j & 3] + pf.pr[j >> 2][j & 3]), 0.f) : 0.f;
+    bf16x8 h, l;
+    split8(v, h, l);
+    const int off = slot * kA1Slot + ((wave * kA1 + pp) * 16 + hh * 8) * 2;
+    *reinterpret_cast<bf16x8*>(a1h + off) = h;
+    *reinterpret_cast<bf16x8*>(a1l + off) = l;
   };
+  // the a1 ring's two pad pixels stay zero
+  for (int e = tid; e < 2 * 3 * 8 * 2 * 2; e += kThreads) {
+    const int pl = e & 1, pad = (e >> 1) & 1, hv = (e >> 2) & 1, b = (e >> 3) % 8, sl = (e >> 3) / 8;
+    const bf16x8 z = {};
+    *reinterpret_cast<bf16x8*>((pl ? a1l : a1h) + sl * kA1Slot + ((b * kA1 + 32 + pad) * 16 + hv * 8) * 2) = z;
+  }
 
-  Pre pf;
-  fetch(y0 - 2, pf);
-  for (int s = y0 - 2; s <= y1 + 1; ++s) {
+  // one output-row step; the a1 table rows are prefetched two steps ahead, alternating between
+  // two register sets (the loop below is unrolled by two so each set keeps its registers)
+  auto step = [&](int s, Pre& pf) {
     // ---- a1 row s
     put_a1(s, pf);
-    if (s + 1 <= y1 + 1) fetch(s + 1, pf);
-    __syncthreads();
+    if (s + 2 <= y1 + 1) fetch(s + 2, pf);
+    lds_barrier();
     const int q = s - 1;  // a2 row
     if (s >= y0) {
       // ---- layer 2, depth block `wave`: 9 taps x 3 products, K = 16 channels each
@@ -313,7 +308,7 @@ __global__ __launch_bounds__(kThreads, 1) void v4_main(Args a) {
         part2[(wave * 32 + m) * 32 + (lane & 31)] = acc[r];
       }
     }
-    __syncthreads();
+    lds_barrier();
     if (s >= y0) {
       // ---- a2 row q = relu(b2 + sum of the 4 depth blocks of its half), masked
       const int m = tid >> 4, g = tid & 15;  // pixel, group of 4 channels (ch = 32 b2 + o2)
@@ -348,7 +343,7 @@ __global__ __launch_bounds__(kThreads, 1) void v4_main(Args a) {
         *reinterpret_cast<bf16x4*>(a2l + off2) = z;
       }
     }
-    __syncthreads();
+    lds_barrier();
     const int r = s - 2;  // output row
     if (s >= y0 + 2) {
       // ---- layer 3: this wave's K steps for its 16-pixel half
@@ -373,7 +368,7 @@ __global__ __launch_bounds__(kThreads, 1) void v4_main(Args a) {
       for (int rr = 0; rr < 4; ++rr)
         part3[(wave * 16 + (lane >> 4) * 4 + rr) * 16 + (lane & 15)] = acc[rr];
     }
-    __syncthreads();
+    lds_barrier();
     if (s >= y0 + 2 && tid < 512) {
       // ---- a3 = relu(b3 + sum over the 4 K groups), out = relu(b4 + w4 . a3), masked
       const int o = tid >> 4, o3 = tid & 15;  // output pixel 0..31, channel
@@ -388,6 +383,13 @@ __global__ __launch_bounds__(kThreads, 1) void v4_main(Args a) {
       const int x = x0 + o;
       if (o3 == 0 && o < kTX && x < W) outp[(int64_t)r * W + x] = x >= i ? fmaxf(v + a.b4[0], 0.f) : 0.f;
     }
+  };
+  Pre pa, pb;
+  fetch(y0 - 2, pa);
+  fetch(y0 - 1, pb);
+  for (int s = y0 - 2; s <= y1 + 1; s += 2) {
+    step(s, pa);
+    if (s + 1 <= y1 + 1) step(s + 1, pb);
   }
 }
 
@@ -423,9 +425,8 @@ int v4_volume_entry(const float* L, const float* R, float* out, int64_t N, int64
   const size_t tables = (size_t)N * H * W * 4 * kCh * sizeof(float);
   __bf16* P2 = reinterpret_cast<__bf16*>(static_cast<unsigned char*>(workspace) + ((tables + 255) / 256) * 256);
   __bf16* P3 = P2 + 2 * (4 * 9 * 64 * 8);
-  const int64_t nthreads = N * H * W * kCh;
-  hipLaunchKernelGGL(v4_tables, dim3((unsigned)ceil_div(nthreads, 256)), dim3(256), 0, st, L, R, ls,
-                     rs, w1, T, (int)N, (int)H, (int)W);
+  hipLaunchKernelGGL(v4_tables, dim3((unsigned)ceil_div(N * H * W, 256), 8), dim3(256), 0, st, L, R,
+                     ls, rs, w1, T, (int)N, (int)H, (int)W);
   rc = check_launch("v4_tables");
   if (rc != SM_OK) return rc;
   hipLaunchKernelGGL(v4_pack, dim3(16), dim3(256), 0, st, w2, w3, P2, P3);
