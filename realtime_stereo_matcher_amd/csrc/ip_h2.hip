@@ -253,14 +253,14 @@ __device__ __forceinline__ float wave_max(float v) {
 // exponent e with x = f 2^e, f in [0.5, 1) (x > 0 finite)
 __device__ __forceinline__ int exp_of(float x) { return __builtin_amdgcn_frexp_expf(x); }
 
-// Workgroups per CU: two (each wave owns 256 registers), except the fused kernels, whose
-// online softmax does not fit beside the accumulators in 256: one, with 512 (VGPRs + AGPRs).
-template <bool FUSE>
+// Workgroups per CU: two (each wave owns 256 registers); the fused kernels too, since their
+// soft-argmin runs on the accumulators themselves before the shear.
+template <int FUSE>
 constexpr int wg_per_cu() {
-  return FUSE ? 1 : 2;
+  return FUSE == 1 ? 1 : 2;
 }
 
-template <typename T, typename TO, int TMAX, bool MEAN, int LAYOUT, bool FUSE>
+template <typename T, typename TO, int TMAX, bool MEAN, int LAYOUT, int FUSE>
 __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args) {
   using G = Geo<T, TMAX>;
   constexpr int DMAX = G::DMAX;
@@ -268,7 +268,7 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
   // The fused kernels run one workgroup per CU with the accumulators partly in AGPRs, where the
   // register allocator splits live ranges with copies: hand-counted asm loads (and L2 touches)
   // are not safe there, so they use compiler-tracked loads.
-  constexpr bool ASM = !FUSE;
+  constexpr bool ASM = FUSE != 1;  // FUSE 1 runs at 512 registers with compiler-tracked loads
   constexpr int PF = ASM ? kPF : 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const T* __restrict__ L = static_cast<const T*>(args.L);
@@ -300,7 +300,7 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
     return wbeg + ((rot && b + 8 <= wcnt) ? (b | ((j + i) & 7)) : j);
   };
   const int nks = (cpg + kKC - 1) / kKC;
-  const bool store_vol = __builtin_amdgcn_readfirstlane(args.out != nullptr ? 1 : 0) != 0;
+  const bool store_vol = FUSE != 2 && __builtin_amdgcn_readfirstlane(args.out != nullptr ? 1 : 0) != 0;
   // NGHWD quads are 16-B aligned only when D % 4 == 0
   const bool dq = LAYOUT == kNDHW || __builtin_amdgcn_readfirstlane(D & 3) == 0;
 
@@ -510,57 +510,86 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
   const int lane_st = LAYOUT == kNDHW ? rl * H * W + 4 * cl : rl * D + 4 * cl;
   const unsigned rdbase = LAYOUT == kNDHW ? ringw + (unsigned)(rl * 128 + 16 * cl)
                                           : ringw + (unsigned)(rl * 384 + 16 * cl);
-  const unsigned colbase = ringw + (unsigned)(16 * hh * 128 + 4 * lr);  // FUSE column reads
 
-  // fused soft-argmin state: pixel lr of the wave, rows 16 hh .. 16 hh + 15 of every chunk (one
-  // pixel per lane: five registers of running state; the two row halves merge at the end)
-  float fm = -INFINITY;
-  double fs = 0.0, ft = 0.0;
-  bool fnan = false;
-  // chunk a's 16 rows of this lane's column, read back from the ring (conflict-free: the 32
-  // lanes of a half read consecutive words), folded into the online softmax
-  auto fuse_chunk = [&](int a, unsigned colb, int Dp, int hho) {
-    float vv[16];
+  // Fused soft-argmin straight from the accumulators: lane (lr, hh) holds, for pixel x0w + lr,
+  // the cells of local disparity dl = 32 (T-1-t) + u - c_i (block t, element i), and the lane
+  // pair (lr, 0), (lr, 1) holds every d of the pixel exactly once.  Pass 1: the pixel's maximum
+  // (and NaN); pass 2: sums of e = exp(v - M) and dl e, fp32 within a block, fp64 across blocks;
+  // the pair merges by one shuffle.  No ring, no LDS: the volume-free kernel never shears.
+  auto fuse_regs = [&](const Work& k, auto scale, auto xlt) {
+    const float mul = args.mul;
+    const int kk = -(kL + kR);
+    const int jlane = k.js + 32 * wave + 4 * hh;
+    const int u0 = lr - 4 * hh;
+    auto value = [&](int t, int i) {
+      const int ci = (i & 3) + 8 * (i >> 2);
+      float val = acc[t][i];
+      if (MEAN) val *= mul;
+      if constexpr (decltype(scale)::value) val = __builtin_ldexpf(val, kk);
+      if constexpr (decltype(xlt)::value) val = jlane + 32 * t + ci >= 0 ? val : 0.f;
+      return val;
+    };
+    // One pass, block by block (every accumulator element read once): the block's maximum, the
+    // running sums rescaled when it grows, the block's exps summed in fp32 and carried into
+    // fp64.  Cells outside 0 <= dl < Dp enter as -inf (e = 0); only the first and the last block
+    // can hold such cells when Dp == DMAX.  No NaN / inf flags: a NaN cell makes its e NaN, a
+    // +inf maximum makes (inf - inf) NaN, an all -inf pixel gives 0 / 0 -- torch's NaN each time.
+    // The shift max(m, -FLT_MAX) keeps exp2 finite-argument when no cell is finite yet.
+    constexpr float kL2E = 1.4426950408889634f;
+    const bool full = k.Dp == DMAX;
+    float m = -INFINITY;
+    double s = 0.0, tt = 0.0;
+    auto block = [&](auto tc, auto maskc) {
+      constexpr int t = decltype(tc)::value;
+      int ub = u0 + 32 * (TMAX - 1 - t);  // dl = ub - c_i; opaque per block (not hoisted)
+      asm volatile("" : "+v"(ub));
+      float v[16];
+      float bm = -INFINITY;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float x = lds_load1(colb + (unsigned)((a % 3) * kSlot + r * 128));
-      vv[r] = 32 * a + 16 * hho + r < Dp ? x : -INFINITY;  // beyond D: not in the softmax
-    }
-    bool nn = false;
-    float cm = -INFINITY;
+      for (int i = 0; i < 16; ++i) {
+        const int ci = (i & 3) + 8 * (i >> 2);
+        float x = value(t, i);
+        if constexpr (decltype(maskc)::value) x = (unsigned)(ub - ci) < (unsigned)k.Dp ? x : -INFINITY;
+        v[i] = x;
+        bm = fmaxf(bm, x);
+      }
+      const float nm = fmaxf(m, bm);
+      const float sh = fmaxf(nm, -3.402823466e38f);
+      const float f = __builtin_amdgcn_exp2f((m - sh) * kL2E);
+      float ps = 0.f, pc = 0.f;  // sum e, sum c_i e
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      nn |= vv[r] != vv[r];
-      cm = fmaxf(cm, vv[r]);
-    }
-    fnan |= nn;
-    const float nm = fmaxf(fm, cm);
-    const bool fin = nm != -INFINITY && nm != INFINITY;
-    // rescale the running sums to the new maximum (factor 1 when it did not grow)
-    const float f = fin && fm != -INFINITY ? expf(fm - nm) : 0.f;
-    float ps = 0.f, pt = 0.f;  // this chunk, disparities relative to its row 32 a + 16 hh
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float ex = fin ? expf(vv[r] - nm) : 0.f;
-      ps += ex;
-      pt = fmaf((float)r, ex, pt);
-    }
-    fs = fs * (double)f + (double)ps;
-    ft = ft * (double)f + (double)(32 * a + 16 * hho) * (double)ps + (double)pt;
-    fm = nm;
-  };
-  auto fuse_finish = [&](const Work& k) {
-    const bool nn2 = __shfl_xor((int)fnan, 32) != 0;  // the other row half of the pixel
-    const float M = fmaxf(fm, __shfl_xor(fm, 32));
-    const double f = (fm == -INFINITY || M == INFINITY) ? 0.0 : (double)expf(fm - M);
-    double s = fs * f, t = ft * f;
+      for (int i = 0; i < 16; ++i) {
+        const float e = __builtin_amdgcn_exp2f((v[i] - sh) * kL2E);
+        ps += e;
+        pc = fmaf((float)((i & 3) + 8 * (i >> 2)), e, pc);
+      }
+      s = s * (double)f + (double)ps;
+      tt = tt * (double)f + (double)ub * (double)ps - (double)pc;  // sum (ub - c_i) e
+      m = nm;
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    // the first and the last block always straddle the band's ends; the middle ones only when
+    // Dp < DMAX (a uniform branch: the common full-D item runs them unmasked)
+    using TT = std::true_type;
+    using FF = std::false_type;
+    [&]<int... T_>(std::integer_sequence<int, T_...>) {
+      ((T_ == 0 || T_ == TMAX - 1
+            ? block(std::integral_constant<int, T_>{}, TT{})
+            : (full ? block(std::integral_constant<int, T_>{}, FF{})
+                    : block(std::integral_constant<int, T_>{}, TT{}))),
+       ...);
+    }(std::make_integer_sequence<int, TMAX>{});
+    // the other row half of the pixel
+    const float M = fmaxf(m, __shfl_xor(m, 32));
+    const double g = (double)__builtin_amdgcn_exp2f((m - fmaxf(M, -3.402823466e38f)) * kL2E);
+    s *= g;
+    tt *= g;
     s += __shfl_xor(s, 32);
-    t += __shfl_xor(t, 32);
-    // NaN anywhere in the column, or an all -inf / any +inf column: NaN, as torch
-    const bool bad = fnan || nn2 || M == INFINITY || M == -INFINITY;
+    tt += __shfl_xor(tt, 32);
+    const bool bad = false;
     const int x = k.x0 + 32 * wave + lr;
     if (hh == 0 && x < W)
-      store_one<float>(args.disp + ((size_t)k.n * H + k.y) * W + x, bad ? NAN : (float)(t / s));
+      store_one<float>(args.disp + ((size_t)k.n * H + k.y) * W + x, bad ? NAN : (float)(tt / s));
   };
 
   // SCALE: multiply back by 2^-(kL+kR); XLT: the segment has cells x < d (R pad rows), forced
@@ -570,11 +599,9 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
     const float mul = args.mul;
     const int kk = -(kL + kR);
     const int jlane = k.js + 32 * wave + 4 * hh;  // R row of element c_i of block 0, minus c_i
-    if constexpr (FUSE) {
-      fm = -INFINITY;
-      fs = 0.0;
-      ft = 0.0;
-      fnan = false;
+    if constexpr (FUSE != 0) {
+      fuse_regs(k, scale, xlt);
+      if (FUSE == 2 || !store_vol) return;  // the volume-free pass: no shear, no ring, no stores
     }
 #pragma unroll
     for (int t = TMAX - 1; t >= 0; --t) {
@@ -582,10 +609,9 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
       // per block, opaque to the compiler: the per-element addresses and selects below are
       // recomputed in each block (two VALU each) instead of being hoisted out of the block loop
       // as 16+ loop-invariant registers (which spill at two workgroups per CU)
-      unsigned wb = wbase, rb = rdbase, cb = colbase;
-      int uu = u, jl = jlane, ls_ = lane_st, rlo = rl, clo = cl, hho = hh;
+      unsigned wb = wbase, rb = rdbase;
+      int uu = u, jl = jlane, ls_ = lane_st, rlo = rl, clo = cl;
       asm volatile("" : "+v"(wb), "+v"(uu), "+v"(jl), "+v"(rb), "+v"(ls_), "+v"(rlo), "+v"(clo));
-      if constexpr (FUSE) asm volatile("" : "+v"(cb), "+v"(hho));
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int ci = (i & 3) + 8 * (i >> 2);
@@ -669,13 +695,9 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
           }
         }
       }
-      if constexpr (FUSE) {
-        if (a >= 0) fuse_chunk(a, cb, k.Dp, hho);
-      }
       // one block at a time (the live accumulators shrink block by block)
       __builtin_amdgcn_sched_barrier(0);
     }
-    if constexpr (FUSE) fuse_finish(k);
   };
 
   auto epilogue = [&](const Work& k, bool fast) {
@@ -724,7 +746,7 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
         }
       }
     }
-    if constexpr (FUSE) {
+    if constexpr (FUSE != 0) {
       for (int xx = tid; xx < kXT; xx += kThreads) {
         const int x = k.x0 + xx;
         if (x >= W) continue;
@@ -766,7 +788,9 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
     if (ks == 0) mx = 0.f;
     __syncthreads();  // A: the previous step's fragment reads are done
     SM_STAMP(0);
-    vm_wait<4 * (TMAX - 1), PF, ASM>(st.v, pfd, __builtin_amdgcn_readfirstlane((int)pend));
+    // after a segment: the volume kernel leaves 4 (T-1) chunk stores in flight, the volume-free
+    // fused kernel its one disparity store per wave
+    vm_wait<FUSE == 2 ? 1 : 4 * (TMAX - 1), PF, ASM>(st.v, pfd, __builtin_amdgcn_readfirstlane((int)pend));
     pend = false;
     put(st);
     const unsigned par = (unsigned)(it & 1) * 8u;
@@ -800,7 +824,7 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
         store_vol && dq && k.x0 + kXT <= W && k.Dp == DMAX && !(SMCV_ABLATE & 12);
     if constexpr (NP == 1) {
       if (!(SMCV_ABLATE & 8)) epilogue(k, fast);
-      pend = fast;  // exactly 4 (T-1) stores per lane were issued after the loads
+      pend = FUSE == 2 ? k.x0 + 32 * wave + 32 <= W : fast;  // as below
       SM_STAMP(4);
       return false;
     } else {
@@ -812,7 +836,9 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
       const bool okr = mr == 0.f || (er + kR <= 15 && er + kR >= -1);
       if (fin && okl && okr) {
         if (!(SMCV_ABLATE & 8)) epilogue(k, fast);
-        pend = fast;  // exactly 4 (T-1) stores per lane were issued after the loads
+        // exactly 4 (T-1) stores per lane were issued after the loads; FUSE 2: one disparity
+        // store per wave, certainly issued when all of the wave's pixels lie inside the row
+        pend = FUSE == 2 ? k.x0 + 32 * wave + 32 <= W : fast;
         SM_STAMP(4);
         redone = false;
         return false;
@@ -884,7 +910,7 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
   SM_STAMP_FLUSH
 }
 
-template <typename T, typename TO, int TMAX, bool MEAN, int LAYOUT, bool FUSE>
+template <typename T, typename TO, int TMAX, bool MEAN, int LAYOUT, int FUSE>
 int launch(Args a, int64_t N, hipStream_t st) {
   using G = Geo<T, TMAX>;
   a.tiles = (int)ceil_div(a.W, kXT);
@@ -1043,8 +1069,13 @@ int band_h2_fused_entry(const void* left, const void* right, void* out, float* d
   hipStream_t st = as_stream(stream);
   return by_tmax(a.pw, [&](auto tm) {
     constexpr int TM = decltype(tm)::value;
-    return mean ? launch<float, float, TM, true, h2band::kNDHW, true>(a, N, st)
-                : launch<float, float, TM, false, h2band::kNDHW, true>(a, N, st);
+    // FUSE 1: volume + disparities (one workgroup per CU, 512 registers); FUSE 2: disparities
+    // only -- no shear, no ring, no volume stores, two workgroups per CU
+    if (out != nullptr)
+      return mean ? launch<float, float, TM, true, h2band::kNDHW, 1>(a, N, st)
+                  : launch<float, float, TM, false, h2band::kNDHW, 1>(a, N, st);
+    return mean ? launch<float, float, TM, true, h2band::kNDHW, 2>(a, N, st)
+                : launch<float, float, TM, false, h2band::kNDHW, 2>(a, N, st);
   });
 }
 
