@@ -257,7 +257,7 @@ __device__ __forceinline__ int exp_of(float x) { return __builtin_amdgcn_frexp_e
 // soft-argmin runs on the accumulators themselves before the shear.
 template <int FUSE>
 constexpr int wg_per_cu() {
-  return FUSE == 1 ? 1 : 2;
+  return 2;
 }
 
 template <typename T, typename TO, int TMAX, bool MEAN, int LAYOUT, int FUSE>
@@ -268,7 +268,7 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
   // The fused kernels run one workgroup per CU with the accumulators partly in AGPRs, where the
   // register allocator splits live ranges with copies: hand-counted asm loads (and L2 touches)
   // are not safe there, so they use compiler-tracked loads.
-  constexpr bool ASM = FUSE != 1;  // FUSE 1 runs at 512 registers with compiler-tracked loads
+  constexpr bool ASM = true;
   constexpr int PF = ASM ? kPF : 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const T* __restrict__ L = static_cast<const T*>(args.L);
@@ -790,7 +790,8 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
     SM_STAMP(0);
     // after a segment: the volume kernel leaves 4 (T-1) chunk stores in flight, the volume-free
     // fused kernel its one disparity store per wave
-    vm_wait<FUSE == 2 ? 1 : 4 * (TMAX - 1), PF, ASM>(st.v, pfd, __builtin_amdgcn_readfirstlane((int)pend));
+    vm_wait<FUSE == 2 ? 1 : 4 * (TMAX - 1) + (FUSE == 1 ? 1 : 0), PF, ASM>(st.v, pfd,
+                                                                     __builtin_amdgcn_readfirstlane((int)pend));
     pend = false;
     put(st);
     const unsigned par = (unsigned)(it & 1) * 8u;
