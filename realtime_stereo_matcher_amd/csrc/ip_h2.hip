@@ -792,6 +792,9 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
     // fused kernel its one disparity store per wave
     vm_wait<FUSE == 2 ? 1 : 4 * (TMAX - 1) + (FUSE == 1 ? 1 : 0), PF, ASM>(st.v, pfd,
                                                                      __builtin_amdgcn_readfirstlane((int)pend));
+#ifdef SMCV_STAMPS
+    if (ks == 0) SM_STAMP(5); else if (ks == 1) SM_STAMP(6); else SM_STAMP(7);
+#endif
     pend = false;
     put(st);
     const unsigned par = (unsigned)(it & 1) * 8u;

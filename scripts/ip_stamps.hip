@@ -115,8 +115,8 @@ int main(int argc, char** argv) {
   }
   if (band) {
     const char* hn[12] = {"barrier waits", "wait+stage (split, lds write)", "load+touch issue",
-                          "frags+mfma", "epilogue (shear, ring, stores)", "-", "-", "-", "-", "-",
-                          "-", "-"};
+                          "frags+mfma", "epilogue (shear, ring, stores)", "vm_wait step 0",
+                          "vm_wait step 1", "vm_wait steps 2+", "-", "-", "-", "-"};
     double sm[12] = {0};
     int n = 0;
     for (int w = 0; w < 4096; ++w) {
