@@ -351,6 +351,39 @@ def cpu_baseline(cfg, a, seconds):
             "ms_per_pair": 1e3 * elapsed / pairs}
 
 
+# ----------------------------------------------------------------------------- PMC traffic
+EVIDENCE_ROUND = "r02"
+
+
+def evidence_name(a):
+    suffix = {"separate": "", "fused": "_fused", "fused-novolume": "_fused_novolume",
+              "interweave": "_interweave"}[a.pipeline]
+    return a.config + suffix
+
+
+def committed_traffic(a, kernel):
+    """HBM bytes per launch of the dominant kernel from the rocprofv3 --pmc FETCH_SIZE /
+    WRITE_SIZE passes of this same command (scripts/gpu_evidence.sh; PMC counters cannot be read
+    in the timed run itself), or None when this workload has no committed counter run."""
+    rel = os.path.join("profiles", EVIDENCE_ROUND, evidence_name(a), "pmc.json")
+    out = {"traffic": None, "traffic_source": None}
+    if a.algo not in ("auto", "h2") or a.batch is not None or a.chunk is not None:
+        return out
+    try:
+        with open(os.path.join(ROOT, rel)) as f:
+            ks = json.load(f)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return out
+    base = kernel.split(" ")[0]
+    cands = [v for k, v in ks.items() if k.startswith(base) and "hbm_bytes_per_launch" in v]
+    if cands:
+        out["traffic"] = round(max(c["hbm_bytes_per_launch"] for c in cands))
+        out["traffic_unit"] = "bytes per launch"
+        out["traffic_source"] = (rel + ": rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate runs "
+                                 "of this command, 2*FETCH_SIZE+WRITE_SIZE (gfx950 correction)")
+    return out
+
+
 # ----------------------------------------------------------------------------- main
 def main():
     a = parse()
@@ -438,12 +471,12 @@ def main():
                    "parallelism": f"dp{world}", "algo": a.algo, "pipeline": a.pipeline,
                    "arithmetic": arithmetic(cfg, a.pipeline, a.algo)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "traffic_note": "PMC HBM bytes are collected in separate rocprofv3 --pmc runs: "
-                                     "profiles/r02_pmc_*.json",
+                     "frac": achieved / HBM_PEAK_GBS,
+                     **committed_traffic(a, kernel_name(cfg, a.pipeline, a.algo)),
                      "kernel": kernel_name(cfg, a.pipeline, a.algo),
                      "avg_kernel_us": 1e3 * kern_ms / launches,
                      "us_per_pair": 1e3 * kern_ms / max(1, timed_pairs),
+                     "algorithmic_bytes_per_launch": nbytes / launches,
                      "algorithmic_bytes_per_pair": pair_bytes(cfg, a.pipeline)},
     }
     if cfg["op"] == "groupwise" and kern_ms > 0:
