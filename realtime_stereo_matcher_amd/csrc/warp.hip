@@ -74,6 +74,34 @@ __global__ __launch_bounds__(kWarpThreads) void warp_kernel(WarpArgs a) {
   const float* ib = a.img + n * a.isn;
   float* ob = a.out + ((int64_t)n * a.C) * HW + p;
   int c = 0;
+  if (a.Wi >= 2) {
+    // The two x-corners of a row are neighbours: one 8-byte (dword-aligned) load per row and
+    // channel, at x0 clamped into [0, Wi-2]; each corner picks its half, or 0 outside the image.
+    // Rows outside the image read row 0 and contribute 0.  Same values, same blend as below.
+    typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
+    const int xc = min(max(x0, 0), a.Wi - 2);
+    const bool r0 = ok[0] || ok[1], r1 = ok[2] || ok[3];  // row y0 / y0+1 inside (x aside)
+    const int64_t o0 = (int64_t)(r0 ? y0 : 0) * a.ish + xc;
+    const int64_t o1 = (int64_t)(r1 ? y0 + 1 : 0) * a.ish + xc;
+    const bool lw = x0 == xc;      // the west corner is the low half (else the high half)
+    const bool le = x0 + 1 == xc;  // the east corner is the low half (x0 = -1)
+    for (; c + kWarpCU <= a.C; c += kWarpCU) {
+      f2u t[kWarpCU], b[kWarpCU];
+#pragma unroll
+      for (int u = 0; u < kWarpCU; ++u) {
+        t[u] = *reinterpret_cast<const f2u*>(ib + (int64_t)(c + u) * a.isc + o0);
+        b[u] = *reinterpret_cast<const f2u*>(ib + (int64_t)(c + u) * a.isc + o1);
+      }
+#pragma unroll
+      for (int u = 0; u < kWarpCU; ++u) {
+        const float v0 = ok[0] ? (lw ? t[u].x : t[u].y) : 0.f;
+        const float v1 = ok[1] ? (le ? t[u].x : t[u].y) : 0.f;
+        const float v2 = ok[2] ? (lw ? b[u].x : b[u].y) : 0.f;
+        const float v3 = ok[3] ? (le ? b[u].x : b[u].y) : 0.f;
+        ob[(int64_t)(c + u) * HW] = v0 * w[0] + v1 * w[1] + v2 * w[2] + v3 * w[3];
+      }
+    }
+  }
   for (; c + kWarpCU <= a.C; c += kWarpCU) {
     float v[kWarpCU][4];
 #pragma unroll
