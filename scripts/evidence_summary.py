@@ -102,8 +102,11 @@ def main():
                 rec = pmc["kernels"].setdefault(k, {})
                 rec.update(c)
                 if c.get("GRBM_GUI_ACTIVE"):
-                    # MFMA busy cycles summed over the 1024 SIMDs vs GPU-active cycles per SIMD
-                    rec["mfma_busy_frac"] = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (1024.0 * c["GRBM_GUI_ACTIVE"])
+                    # SQ_VALU_MFMA_BUSY_CYCLES is summed over all 1024 SIMDs (32 cycles per
+                    # 32x32x16 MFMA, MI355X_MICROARCH.md); GRBM_GUI_ACTIVE is summed over the 8
+                    # XCDs (8 x kernel cycles), so the busy fraction per SIMD is
+                    # MFMA_BUSY / (1024 * GRBM_GUI_ACTIVE / 8)
+                    rec["mfma_busy_frac"] = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (128.0 * c["GRBM_GUI_ACTIVE"])
         json.dump(pmc, open(os.path.join(dst, "pmc.json"), "w"), indent=1)
         for k, rec in pmc["kernels"].items():
             if row.get("rocprof_top_kernel") == k:
