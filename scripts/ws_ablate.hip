@@ -1,7 +1,7 @@
 // Diagnostic driver: median kernel time (HIP events) of one band-kernel launch on the cfg2 shape
 // (1x64x540x960 fp32, D=192) for ablation builds of csrc/ip_ws.hip.  Build + run on the GPU box:
 //   hipcc -O3 -std=c++20 --offload-arch=gfx950 -DSMCV_ABLATE=N -Iinclude scripts/ws_ablate.hip -o /tmp/wsa && /tmp/wsa [mode]
-// modes: ws (default), wsfused, wsfusednv, wsgw (cfg3 bf16 groupwise), h2
+// modes: ws (default), wsfused, wsfusednv, wsgw (cfg3 bf16 groupwise), h2, h2fused, h2fusednv
 #include "../realtime_stereo_matcher_amd/csrc/common.hip"
 #include "../realtime_stereo_matcher_amd/csrc/cv_dot.hip"
 #include "../realtime_stereo_matcher_amd/csrc/ip_h2.hip"
@@ -42,6 +42,9 @@ int main(int argc, char** argv) {
   bool handled = false;
   auto run = [&]() {
     if (!strcmp(mode, "h2")) return smcv::band_h2_entry(L, R, O, SM_F32, N, C, H, W, D, nullptr, nullptr, 0, nullptr, &handled);
+    if (!strcmp(mode, "h2fused") || !strcmp(mode, "h2fusednv"))
+      return smcv::band_h2_fused_entry(L, R, !strcmp(mode, "h2fused") ? O : nullptr, disp, SM_F32, N, C, H, W, D,
+                                       nullptr, nullptr, 0, nullptr, &handled);
     if (!strcmp(mode, "wsfused") || !strcmp(mode, "wsfusednv"))
       return smcv::band_ws_fused_entry(L, R, !strcmp(mode, "wsfused") ? O : nullptr, disp, SM_F32, N, C, H, W, D,
                                        nullptr, nullptr, 0, nullptr, &handled);
