@@ -331,9 +331,12 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
     const int cl = ks * kKC + 8 * ch;  // channel within the group
     const int px = isR ? k.js + 4 * g : k.x0 + 4 * g - G::RW;
     const bool okp = active && px >= 0 && px < W;
-    const T* p = row_of(k) + (okp ? px : 0) + ((int64_t)k.g * cpg + min(cl, cpg - 1)) * cs;
+    // W % 4 != 0 (fp32 only): the group holding a row's end reads the row's last 4 pixels
+    // (W - 4 .. W - 1, in bounds) and put() moves its W % 4 valid pixels down; flagged in nv
+    const bool strad = NP == 2 && okp && px + 4 > W;
+    const T* p = row_of(k) + (okp ? (strad ? W - 4 : px) : 0) + ((int64_t)k.g * cpg + min(cl, cpg - 1)) * cs;
     if (SMCV_ABLATE & 2) p = L + 4 * (lane & 7);
-    st.nv = okp ? min(max(cpg - cl, 0), 8) : 0;
+    st.nv = (okp ? min(max(cpg - cl, 0), 8) : 0) | (strad ? 16 : 0);
     // channel tail: clamp to the group's last channel (one code path; put() zeroes the tail)
     const int lim = cfull ? 7 : min(max(cpg - 1 - cl, 0), 7);
     // the channel stride, opaque here: the 8 addresses are stepped, not 8 hoisted 64-bit offsets
@@ -371,9 +374,20 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
       for (int kk = 0; kk < 8; ++kk)
         v[kk] = make_float4(st.v[kk].x, st.v[kk].y, st.v[kk].z, st.v[kk].w);
       if (__any(st.nv != 8)) {  // row edges / channel tail only
+        const int nv = st.nv & 15;
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk)
-          if (kk >= st.nv) v[kk] = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (kk >= nv) v[kk] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (st.nv & 16) {  // loaded from W - 4: pixels W - r .. W - 1 move to lanes' slots 0 .. r-1
+          const int r = W & 3;
+#pragma unroll
+          for (int kk = 0; kk < 8; ++kk) {
+            const float4 o = v[kk];
+            v[kk] = r == 1 ? make_float4(o.w, 0.f, 0.f, 0.f)
+                  : r == 2 ? make_float4(o.z, o.w, 0.f, 0.f)
+                           : make_float4(o.y, o.z, o.w, 0.f);
+          }
+        }
       }
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk)
@@ -667,7 +681,16 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
               for (int qq = 0; qq < 4; ++qq) {
                 asm volatile("" : "+v"(ol));
                 const int dl = 32 * a + 8 * qq + rlo;
-                if (dl < k.Dp && x0w + 4 * clo < W && !(SMCV_ABLATE & 4)) store_quad<TO>(ol, v[qq]);
+                const int xq = x0w + 4 * clo;
+                if (dl < k.Dp && xq < W && !(SMCV_ABLATE & 4)) {
+                  if (xq + 4 <= W) {
+                    store_quad<TO>(ol, v[qq]);
+                  } else {  // the row's last, partial quad (W % 4 != 0)
+#pragma unroll
+                    for (int e = 0; e < 3; ++e)
+                      if (xq + e < W) store_one<TO>(ol + e, v[qq][e]);
+                  }
+                }
                 ol += st8;
               }
             }
@@ -957,10 +980,15 @@ int h2_prepare(const void* left, const void* right, const void* out, int dtype, 
   int rc = check_dot_args(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, &ls, &rs);
   if (rc) return rc;
   const uintptr_t align = 4 * (uintptr_t)elem_size(dtype);
-  *vec = (W % 4 == 0) && W >= 4 && C > 0 && ls.n % 4 == 0 && ls.c % 4 == 0 && ls.h % 4 == 0 &&
-         rs.n % 4 == 0 && rs.c % 4 == 0 && rs.h % 4 == 0 &&
-         ((reinterpret_cast<uintptr_t>(left) | reinterpret_cast<uintptr_t>(right)) % align == 0) &&
-         reinterpret_cast<uintptr_t>(out) % 16 == 0 && 8 * H * W < INT32_MAX &&
+  const bool aligned4 = (W % 4 == 0) && ls.n % 4 == 0 && ls.c % 4 == 0 && ls.h % 4 == 0 &&
+                       rs.n % 4 == 0 && rs.c % 4 == 0 && rs.h % 4 == 0 &&
+                       ((reinterpret_cast<uintptr_t>(left) | reinterpret_cast<uintptr_t>(right)) % align == 0) &&
+                       reinterpret_cast<uintptr_t>(out) % 16 == 0;
+  // fp32 rows of any width (and any element strides): the 16-B feature loads and volume stores
+  // are then only dword-aligned, which gfx950 global memory accesses allow (unaligned mode);
+  // the row-end group is handled in load() / put() and the row-end quad in the epilogue
+  const bool any_w = dtype == SM_F32 && reinterpret_cast<uintptr_t>(out) % 4 == 0;
+  *vec = (aligned4 || any_w) && W >= 4 && C > 0 && 8 * H * W < INT32_MAX &&
          8 * W * std::max<int64_t>(D, 1) < INT32_MAX;
   // D passes of at most 192 disparities, balanced (D = 256: two passes of 128); a pass width
   // that is a multiple of 4 keeps every right-window pixel group aligned
