@@ -202,14 +202,16 @@ __device__ __forceinline__ void vm_wait(QT (&v)[8], unsigned& pf, int after_stor
 // 4 fp32 results -> storage type (round to nearest even; NaN stays NaN, overflow gives inf).
 // Global address space explicitly: a flat store would count in vmcnt out of order.
 template <typename T>
-__device__ __forceinline__ void store_quad(T* p, f32x4v v) {
+__device__ __forceinline__ void store_quad(T* p, f32x4v v, bool nt = true) {
   typedef __attribute__((address_space(1))) void gvoid;
   gvoid* g = (gvoid*)p;
   // non-temporal: the volume is written once and never re-read by this kernel; plain stores
   // would allocate its lines in L2 and evict the feature lines the loads reuse
-  // (scripts/micro/mlp_patterns.hip: cfg2 reads + writes 140 us plain vs 106 us nt)
+  // (scripts/micro/mlp_patterns.hip: cfg2 reads + writes 140 us plain vs 106 us nt).
+  // nt == false (fp32 rows with W % 4 != 0, whose 128-B row pieces straddle two lines): plain
+  // stores, so that L2 merges the two halves of a line before it writes the line back.
   if constexpr (sizeof(T) == 4) {
-    if (SMCV_NT_STORE)
+    if (SMCV_NT_STORE && nt)
       __builtin_nontemporal_store(v, reinterpret_cast<__attribute__((address_space(1))) f32x4v*>(g));
     else
       *reinterpret_cast<__attribute__((address_space(1))) f32x4v*>(g) = v;
@@ -519,6 +521,7 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
                                          : ringw + (unsigned)(384 * lr + 4 * u);
   const int rl = lane >> 3, cl = lane & 7;  // chunk readout: rows (NDHW) / pixels (NGHWD) 8qq + rl
   const size_t plane_stride = (size_t)H * W;
+  const bool ntq = __builtin_amdgcn_readfirstlane(W & 3) == 0;  // see store_quad
   // lane parts of the chunk store addresses, in elements (32-bit: the host keeps 8 H W < 2^31);
   // the rest of each address is uniform (scalar registers)
   const int lane_st = LAYOUT == kNDHW ? rl * H * W + 4 * cl : rl * D + 4 * cl;
@@ -673,7 +676,7 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
 #pragma unroll
               for (int qq = 0; qq < 4; ++qq) {
                 asm volatile("" : "+v"(ol));
-                store_quad<TO>(ol, v[qq]);
+                store_quad<TO>(ol, v[qq], ntq);
                 ol += st8;
               }
             } else {
@@ -684,7 +687,7 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
                 const int xq = x0w + 4 * clo;
                 if (dl < k.Dp && xq < W && !(SMCV_ABLATE & 4)) {
                   if (xq + 4 <= W) {
-                    store_quad<TO>(ol, v[qq]);
+                    store_quad<TO>(ol, v[qq], ntq);
                   } else {  // the row's last, partial quad (W % 4 != 0)
 #pragma unroll
                     for (int e = 0; e < 3; ++e)
