@@ -1,7 +1,7 @@
 // Diagnostic driver: median kernel time (HIP events) of one band-kernel launch on the cfg2 shape
 // (1x64x540x960 fp32, D=192) for ablation builds of csrc/ip_ws.hip.  Build + run on the GPU box:
 //   hipcc -O3 -std=c++20 --offload-arch=gfx950 -DSMCV_ABLATE=N -Iinclude scripts/ws_ablate.hip -o /tmp/wsa && /tmp/wsa [mode]
-// modes: ws (default), wsfused, wsfusednv, wsgw (cfg3 bf16 groupwise), h2, h2fused, h2fusednv
+// modes: ws (default), wsfused, wsfusednv, wsgw (cfg3 bf16 groupwise), h2, h2fused, h2fusednv, h2gw (cfg3), h2corr4 (cfg4 one pair)
 #include "../realtime_stereo_matcher_amd/csrc/common.hip"
 #include "../realtime_stereo_matcher_amd/csrc/cv_dot.hip"
 #include "../realtime_stereo_matcher_amd/csrc/ip_h2.hip"
@@ -14,8 +14,10 @@
 
 int main(int argc, char** argv) {
   const char* mode = argc > 1 ? argv[1] : "ws";
-  const bool gw = !strcmp(mode, "wsgw");
-  const int64_t N = 1, C = gw ? 256 : 64, H = 540, W = 960, D = 192, G = 8;
+  const bool gw = !strcmp(mode, "wsgw") || !strcmp(mode, "h2gw");
+  const bool c4 = !strcmp(mode, "h2corr4");  // cfg4: 1x16x1080x1920 fp32, correlation D=256
+  const int64_t N = 1, C = gw ? 256 : c4 ? 16 : 64, H = c4 ? 1080 : 540, W = c4 ? 1920 : 960,
+                D = c4 ? 256 : 192, G = 8;
   const size_t nin = N * C * H * W, nout = gw ? N * G * H * W * D : N * D * H * W;
   const size_t esz = gw ? 2 : 4;
   void *L, *R;
@@ -41,6 +43,9 @@ int main(int argc, char** argv) {
   }
   bool handled = false;
   auto run = [&]() {
+    if (!strcmp(mode, "h2gw"))
+      return smcv::band_h2_groupwise_entry(L, R, O, SM_BF16, N, C, H, W, D, G, nullptr, nullptr, nullptr, &handled);
+    if (c4) return smcv::band_h2_entry(L, R, O, SM_F32, N, C, H, W, D, nullptr, nullptr, 1, nullptr, &handled);
     if (!strcmp(mode, "h2")) return smcv::band_h2_entry(L, R, O, SM_F32, N, C, H, W, D, nullptr, nullptr, 0, nullptr, &handled);
     if (!strcmp(mode, "h2fused") || !strcmp(mode, "h2fusednv"))
       return smcv::band_h2_fused_entry(L, R, !strcmp(mode, "h2fused") ? O : nullptr, disp, SM_F32, N, C, H, W, D,
