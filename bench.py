@@ -361,13 +361,14 @@ def evidence_name(a):
     return a.config + suffix
 
 
-def committed_traffic(a, kernel):
+def committed_traffic(a, kernel, world=1):
     """HBM bytes per launch of the dominant kernel from the rocprofv3 --pmc FETCH_SIZE /
     WRITE_SIZE passes of this same command (scripts/gpu_evidence.sh; PMC counters cannot be read
     in the timed run itself), or None when this workload has no committed counter run."""
     rel = os.path.join("profiles", EVIDENCE_ROUND, evidence_name(a), "pmc.json")
     out = {"traffic": None, "traffic_source": None}
-    if a.algo not in ("auto", "h2") or a.batch is not None or a.chunk is not None:
+    # the committed passes ran this workload at N=1 with the default pairs per launch
+    if a.algo not in ("auto", "h2") or a.batch is not None or a.chunk is not None or world != 1:
         return out
     try:
         with open(os.path.join(ROOT, rel)) as f:
@@ -472,7 +473,7 @@ def main():
                    "arithmetic": arithmetic(cfg, a.pipeline, a.algo)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
-                     **committed_traffic(a, kernel_name(cfg, a.pipeline, a.algo)),
+                     **committed_traffic(a, kernel_name(cfg, a.pipeline, a.algo), world),
                      "kernel": kernel_name(cfg, a.pipeline, a.algo),
                      "avg_kernel_us": 1e3 * kern_ms / launches,
                      "us_per_pair": 1e3 * kern_ms / max(1, timed_pairs),
