@@ -16,7 +16,8 @@ int main(int argc, char** argv) {
   const char* mode = argc > 1 ? argv[1] : "ws";
   const bool gw = !strcmp(mode, "wsgw") || !strcmp(mode, "h2gw");
   const bool c4 = !strcmp(mode, "h2corr4");  // cfg4: 1x16x1080x1920 fp32, correlation D=256
-  const int64_t N = 1, C = gw ? 256 : c4 ? 16 : 64, H = c4 ? 1080 : 540, W = c4 ? 1920 : 960,
+  const bool x8 = !strcmp(mode, "h2x8");  // cfg2, 8 pairs per launch (the bench's chunk)
+  const int64_t N = x8 ? 8 : 1, C = gw ? 256 : c4 ? 16 : 64, H = c4 ? 1080 : 540, W = c4 ? 1920 : 960,
                 D = c4 ? 256 : 192, G = 8;
   const size_t nin = N * C * H * W, nout = gw ? N * G * H * W * D : N * D * H * W;
   const size_t esz = gw ? 2 : 4;
@@ -46,7 +47,7 @@ int main(int argc, char** argv) {
     if (!strcmp(mode, "h2gw"))
       return smcv::band_h2_groupwise_entry(L, R, O, SM_BF16, N, C, H, W, D, G, nullptr, nullptr, nullptr, &handled);
     if (c4) return smcv::band_h2_entry(L, R, O, SM_F32, N, C, H, W, D, nullptr, nullptr, 1, nullptr, &handled);
-    if (!strcmp(mode, "h2")) return smcv::band_h2_entry(L, R, O, SM_F32, N, C, H, W, D, nullptr, nullptr, 0, nullptr, &handled);
+    if (!strcmp(mode, "h2") || x8) return smcv::band_h2_entry(L, R, O, SM_F32, N, C, H, W, D, nullptr, nullptr, 0, nullptr, &handled);
     if (!strcmp(mode, "h2fused") || !strcmp(mode, "h2fusednv"))
       return smcv::band_h2_fused_entry(L, R, !strcmp(mode, "h2fused") ? O : nullptr, disp, SM_F32, N, C, H, W, D,
                                        nullptr, nullptr, 0, nullptr, &handled);
