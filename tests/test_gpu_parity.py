@@ -182,6 +182,9 @@ SHAPES = [  # (N, C, H, W, D)
     # W % 4 == 0 shapes for the 16-B staging paths: channel tails, partial bands, D passes, W < 128
     (2, 20, 3, 260, 100), (1, 48, 2, 132, 33), (1, 16, 1, 1000, 256), (1, 7, 2, 36, 40),
     (1, 64, 2, 960, 192), (1, 33, 2, 512, 31),
+    # fp32 rows of width W % 4 != 0 on the band kernel: misaligned 16-B loads / stores, the
+    # row-end group loaded from W - 4, full tiles (plain stores) and a partial last quad
+    (1, 64, 2, 958, 192), (2, 24, 2, 257, 100), (1, 64, 1, 957, 64),
 ]
 
 
@@ -612,7 +615,8 @@ def test_groupwise_band_nonfinite():
 
 
 FUSED_SHAPES = [(1, 64, 3, 512, 192), (2, 20, 3, 260, 100), (1, 33, 2, 132, 31), (1, 16, 2, 64, 64),
-                (1, 8, 3, 100, 24), (1, 7, 2, 36, 40), (1, 16, 2, 64, 256), (1, 5, 2, 33, 9)]
+                (1, 8, 3, 100, 24), (1, 7, 2, 36, 40), (1, 16, 2, 64, 256), (1, 5, 2, 33, 9),
+                (1, 64, 2, 958, 192), (2, 20, 2, 259, 100)]
 
 
 @pytest.mark.parametrize("mean", [False, True])
@@ -620,7 +624,8 @@ FUSED_SHAPES = [(1, 64, 3, 512, 192), (2, 20, 3, 260, 100), (1, 33, 2, 132, 31),
 def test_fused_soft_argmin(shape, mean):
     """Volume + soft-argmin in one pass: the volume is bit-identical to the
     volume op's, the disparity is the fp64 soft-argmin of that volume within 1e-4, and the
-    volume-free call returns the same disparity (D > 192 or W % 4 != 0: two kernels)."""
+    volume-free call returns the same disparity (D > 192: two kernels; fp32 rows of any width
+    take the fused kernel)."""
     from realtime_stereo_matcher_amd import functional as F
 
     n, c, h, w, D = shape
