@@ -161,6 +161,8 @@ def make_step(cfg, a, L, R, ev):
             vol, disp = F.inner_product_soft_argmin(l, r, D, keep_volume=a.pipeline == "fused")
             return vol, disp
         if cfg["op"] == "correlation":
+            if a.pipeline.startswith("fused"):  # D = 256 volume-free: 2 passes + merge
+                return F.inner_product_soft_argmin(l, r, D, mean=True, keep_volume=a.pipeline == "fused")
             return F.correlation_volume(l, r, D), None
         if cfg["op"] == "groupwise":
             return F.groupwise_volume(l, r, cfg["G"], D), None
@@ -389,8 +391,8 @@ def committed_traffic(a, kernel, world=1):
 def main():
     a = parse()
     cfg = CONFIGS[a.config]
-    if a.pipeline in ("fused", "fused-novolume") and cfg["op"] != "inner_product":
-        raise SystemExit("--pipeline fused* applies to cfg2 (fused inner product + soft-argmin)")
+    if a.pipeline in ("fused", "fused-novolume") and cfg["op"] not in ("inner_product", "correlation"):
+        raise SystemExit("--pipeline fused* applies to cfg2 / cfg4 (fused volume + soft-argmin)")
     if a.pipeline == "interweave" and cfg["op"] != "concat":
         raise SystemExit("--pipeline interweave applies to cfg5")
     if a.pipeline != "separate" and a.algo not in ("auto", "h2"):

@@ -89,8 +89,8 @@ int sm_cv_correlation_mean(const void* left, const void* right, void* out, int d
  *   disparity_regression -- model/mobile_disp_net_c.py:208-220 (= the inline soft-argmin of
  *   model/mobile_stereo_net.py:144-147).
  * disparity[n,y,x] = sum_d d * softmax_d(vol[n,:,y,x]): (N, H, W) in `dtype`; the (N, D, H, W)
- * volume is written too when out_volume != NULL.  fp32 features with W % 4 == 0, 16-B aligned
- * rows and D <= 192 take the fused band kernel (the volume is never read back; with
+ * volume is written too when out_volume != NULL.  fp32 features (W >= 4) with D <= 192 take
+ * the fused band kernel (the volume is never read back; with
  * out_volume == NULL it is never written).  Other shapes run the volume and the regression as
  * two kernels, which needs out_volume: with out_volume == NULL they return SM_EUNSUPPORTED.
  * D == 0: the disparity is 0 (an empty softmax axis). */
@@ -98,6 +98,19 @@ int sm_cv_inner_product_softargmin(const void* left, const void* right, void* ou
                                    void* disparity, int dtype, int64_t N, int64_t C, int64_t H,
                                    int64_t W, int64_t D, const int64_t* l_strides,
                                    const int64_t* r_strides, int mode, void* stream);
+
+/* f-1 for D > 192 without the volume (e.g. make_correlation_volume + disparity_regression of
+ * MobileDispNetC at D = 256, model/mobile_disp_net_c.py:188-220): the band kernel runs D in
+ * passes of <= 192 disparities, each pass writes its partial softmax state per pixel into a
+ * caller-provided device workspace (8-byte aligned, at least
+ * sm_cv_inner_product_softargmin_workspace_bytes(N, H, W, D) bytes; 0 for D <= 192) and a
+ * second kernel merges them.  Otherwise as sm_cv_inner_product_softargmin. */
+int64_t sm_cv_inner_product_softargmin_workspace_bytes(int64_t N, int64_t H, int64_t W, int64_t D);
+int sm_cv_inner_product_softargmin_ws(const void* left, const void* right, void* out_volume,
+                                      void* disparity, int dtype, int64_t N, int64_t C,
+                                      int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
+                                      const int64_t* r_strides, int mode, void* workspace,
+                                      int64_t workspace_bytes, void* stream);
 
 /* a-2: TorchGroupwiseCost(n_groups, max_disparity)(left, right)
  *      -- cost_volume/groupwise.py:24-56

@@ -30,6 +30,8 @@ SIGNATURES = {
     "sm_cv_correlation_mean": [_p, _p, _p, _i, _l, _l, _l, _l, _l, _lp, _lp, _p],
     "sm_cv_groupwise": [_p, _p, _p, _i, _l, _l, _l, _l, _l, _l, _lp, _lp, _p],
     "sm_cv_inner_product_softargmin": [_p, _p, _p, _p, _i, _l, _l, _l, _l, _l, _lp, _lp, _i, _p],
+    "sm_cv_inner_product_softargmin_workspace_bytes": [_l, _l, _l, _l],
+    "sm_cv_inner_product_softargmin_ws": [_p, _p, _p, _p, _i, _l, _l, _l, _l, _l, _lp, _lp, _i, _p, _l, _p],
     "sm_cv_concat": [_p, _p, _p, _i, _l, _l, _l, _l, _l, _lp, _lp, _p],
     "sm_cv_interweave": [_p, _p, _p, _i, _l, _l, _l, _l, _lp, _lp, _p],
     "sm_cv_interweave_shifted": [_p, _p, _p, _i, _l, _l, _l, _l, _l, _lp, _lp, _p],
@@ -40,7 +42,8 @@ SIGNATURES = {
     "sm_v4_volume_workspace_bytes": [_l, _l, _l],
     "sm_v4_volume": [_p, _p, _p, _i, _l, _l, _l, _l, _l, _lp, _lp] + [_p] * 9 + [_l, _p],
 }
-_RESTYPE = {"sm_last_error": ctypes.c_char_p, "sm_v4_volume_workspace_bytes": ctypes.c_int64}
+_RESTYPE = {"sm_last_error": ctypes.c_char_p, "sm_v4_volume_workspace_bytes": ctypes.c_int64,
+            "sm_cv_inner_product_softargmin_workspace_bytes": ctypes.c_int64}
 
 _lock = threading.Lock()
 _lib = None

@@ -22,7 +22,8 @@ int band_h2_groupwise_entry(const void* left, const void* right, float* out, int
 int band_h2_fused_entry(const void* left, const void* right, void* out, float* disp, int dtype,
                         int64_t N, int64_t C, int64_t H, int64_t W, int64_t D,
                         const int64_t* l_strides, const int64_t* r_strides, int mode,
-                        void* stream, bool* handled);
+                        void* stream, bool* handled, void* workspace, int64_t ws_bytes);
+int64_t band_h2_fused_workspace_bytes(int64_t N, int64_t H, int64_t W, int64_t D);
 size_t v4_workspace_bytes(int64_t N, int64_t H, int64_t W);
 int v4_volume_entry(const float* L, const float* R, float* out, int64_t N, int64_t C, int64_t H,
                     int64_t W, int64_t D, const int64_t* l_strides, const int64_t* r_strides,
@@ -143,14 +144,14 @@ extern "C" int sm_cv_groupwise(const void* left, const void* right, float* out, 
                                2, stream);
 }
 
-extern "C" int sm_cv_inner_product_softargmin(const void* left, const void* right,
-                                              void* out_volume, void* disparity, int dtype,
-                                              int64_t N, int64_t C, int64_t H, int64_t W,
-                                              int64_t D, const int64_t* l_strides,
-                                              const int64_t* r_strides, int mode, void* stream) {
-  SM_ENTRY_BEGIN
+namespace {
+int fused_softargmin(const void* left, const void* right, void* out_volume, void* disparity,
+                     int dtype, int64_t N, int64_t C, int64_t H, int64_t W, int64_t D,
+                     const int64_t* l_strides, const int64_t* r_strides, int mode,
+                     void* workspace, int64_t ws_bytes, void* stream) {
   if (mode != 0 && mode != 1) return fail(SM_EINVAL, "mode must be 0 (sum) or 1 (mean)");
   if (!valid_dtype(dtype)) return fail(SM_EDTYPE, "unsupported dtype code");
+  if (ws_bytes < 0) return fail(SM_EINVAL, "negative workspace size");
   if (D == 0 && N * H * W > 0) {  // softmax over an empty axis: the weighted sum is 0
     if (disparity == nullptr) return fail(SM_EINVAL, "null disparity pointer");
     const hipError_t e = hipMemsetAsync(disparity, 0, (size_t)(N * H * W) * elem_size(dtype),
@@ -159,12 +160,14 @@ extern "C" int sm_cv_inner_product_softargmin(const void* left, const void* righ
   }
   bool handled = false;
   int rc = band_h2_fused_entry(left, right, out_volume, static_cast<float*>(disparity), dtype, N,
-                               C, H, W, D, l_strides, r_strides, mode, stream, &handled);
+                               C, H, W, D, l_strides, r_strides, mode, stream, &handled,
+                               workspace, ws_bytes);
   if (handled || rc != SM_OK) return rc;
   if (out_volume == nullptr)
     return fail(SM_EUNSUPPORTED,
-                "fused cost volume + soft-argmin needs fp32 features, W % 4 == 0, 16-B aligned "
-                "rows and D <= 192; pass a volume buffer for the two-kernel path");
+                "fused cost volume + soft-argmin needs fp32 features (W >= 4) and D <= 192, or a "
+                "workspace of sm_cv_inner_product_softargmin_workspace_bytes() for D > 192; pass "
+                "a volume buffer for the two-kernel path");
   rc = mode == 1 ? sm_cv_correlation_mean(left, right, out_volume, dtype, N, C, H, W, D,
                                           l_strides, r_strides, stream)
                  : sm_cv_inner_product(left, right, out_volume, dtype, N, C, H, W, D, l_strides,
@@ -172,6 +175,35 @@ extern "C" int sm_cv_inner_product_softargmin(const void* left, const void* righ
   if (rc != SM_OK) return rc;
   return softargmin_entry(out_volume, disparity, dtype, N, D, H, W, SM_REGRESS_SOFTMAX, nullptr,
                           stream);
+}
+}  // namespace
+
+extern "C" int sm_cv_inner_product_softargmin(const void* left, const void* right,
+                                              void* out_volume, void* disparity, int dtype,
+                                              int64_t N, int64_t C, int64_t H, int64_t W,
+                                              int64_t D, const int64_t* l_strides,
+                                              const int64_t* r_strides, int mode, void* stream) {
+  SM_ENTRY_BEGIN
+  return fused_softargmin(left, right, out_volume, disparity, dtype, N, C, H, W, D, l_strides,
+                          r_strides, mode, nullptr, 0, stream);
+}
+
+extern "C" int64_t sm_cv_inner_product_softargmin_workspace_bytes(int64_t N, int64_t H, int64_t W,
+                                                                  int64_t D) {
+  if (N < 0 || H < 0 || W < 0 || D < 0) return 0;
+  return band_h2_fused_workspace_bytes(N, H, W, D);
+}
+
+extern "C" int sm_cv_inner_product_softargmin_ws(const void* left, const void* right,
+                                                 void* out_volume, void* disparity, int dtype,
+                                                 int64_t N, int64_t C, int64_t H, int64_t W,
+                                                 int64_t D, const int64_t* l_strides,
+                                                 const int64_t* r_strides, int mode,
+                                                 void* workspace, int64_t workspace_bytes,
+                                                 void* stream) {
+  SM_ENTRY_BEGIN
+  return fused_softargmin(left, right, out_volume, disparity, dtype, N, C, H, W, D, l_strides,
+                          r_strides, mode, workspace, workspace_bytes, stream);
 }
 
 extern "C" int sm_cv_concat(const void* left, const void* right, void* out, int dtype, int64_t N,

@@ -116,10 +116,16 @@ struct Args {
   Strides4 ls, rs;
   int tiles, npass, pw, nwork;
   float mul;  // MEAN: 1 / (channels averaged)
+  // volume-free fused kernel with npass > 1: each pass's partial soft-argmin state per pixel
+  // (max, sum e, sum d e relative to that max), merged by fused_merge_kernel
+  double* ws_s;
+  double* ws_t;
+  float* ws_m;
+  int64_t nhw;  // N H W: the workspace's per-pass stride
 };
 
 struct Work {
-  int n, y, g, x0, dp, Dp, js;
+  int n, y, g, x0, dp, Dp, js, pass;
 };
 
 // work index w = (((n H + y) G + g) tiles + tile) npass + pass: consecutive items are
@@ -136,6 +142,7 @@ __device__ __forceinline__ Work decode(int w, const Args& a, int dmax) {
   k.n = row / a.H;
   k.x0 = tile * kXT;
   k.dp = pass * a.pw;
+  k.pass = pass;
   k.Dp = min(a.pw, a.D - k.dp);
   k.js = k.x0 - k.dp - dmax;
   return k;
@@ -603,10 +610,20 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
     tt *= g;
     s += __shfl_xor(s, 32);
     tt += __shfl_xor(tt, 32);
-    const bool bad = false;
     const int x = k.x0 + 32 * wave + lr;
-    if (hh == 0 && x < W)
-      store_one<float>(args.disp + ((size_t)k.n * H + k.y) * W + x, bad ? NAN : (float)(tt / s));
+    if (hh == 0 && x < W) {
+      const size_t px = ((size_t)k.n * H + k.y) * W + x;
+      if (args.ws_m != nullptr) {  // one of several D passes: its partial state, d global
+        typedef __attribute__((address_space(1))) void gvoid;
+        const size_t o = (size_t)k.pass * ((size_t)args.nhw) + px;
+        *reinterpret_cast<__attribute__((address_space(1))) double*>((gvoid*)(args.ws_s + o)) = s;
+        *reinterpret_cast<__attribute__((address_space(1))) double*>((gvoid*)(args.ws_t + o)) =
+            tt + (double)k.dp * s;
+        store_one<float>(args.ws_m + o, M);
+      } else {
+        store_one<float>(args.disp + px, (float)(tt / s));
+      }
+    }
   };
 
   // SCALE: multiply back by 2^-(kL+kR); XLT: the segment has cells x < d (R pad rows), forced
@@ -940,6 +957,27 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
   SM_STAMP_FLUSH
 }
 
+// Merge of the per-pass partial soft-argmin states (volume-free fused kernel, D > 192): the
+// same shift-and-rescale as the lane-pair merge inside the band kernel, over the passes.
+__global__ __launch_bounds__(256) void fused_merge_kernel(const double* __restrict__ S,
+                                                          const double* __restrict__ T,
+                                                          const float* __restrict__ Mv, int npass,
+                                                          int64_t nhw, float* __restrict__ disp) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nhw) return;
+  constexpr float kL2E = 1.4426950408889634f;
+  float M = -INFINITY;
+  for (int p = 0; p < npass; ++p) M = fmaxf(M, Mv[p * nhw + i]);
+  const float sh = fmaxf(M, -3.402823466e38f);
+  double s = 0.0, t = 0.0;
+  for (int p = 0; p < npass; ++p) {
+    const double g = (double)__builtin_amdgcn_exp2f((Mv[p * nhw + i] - sh) * kL2E);
+    s += S[p * nhw + i] * g;
+    t += T[p * nhw + i] * g;
+  }
+  disp[i] = (float)(t / s);
+}
+
 template <typename T, typename TO, int TMAX, bool MEAN, int LAYOUT, int FUSE>
 int launch(Args a, int64_t N, hipStream_t st) {
   using G = Geo<T, TMAX>;
@@ -1014,6 +1052,9 @@ int h2_prepare(const void* left, const void* right, const void* out, int dtype, 
   a->pw = (int)pw;
   a->nwork = 0;
   a->mul = 1.0f;
+  a->ws_s = a->ws_t = nullptr;
+  a->ws_m = nullptr;
+  a->nhw = N * H * W;
   return SM_OK;
 }
 }  // namespace
@@ -1077,10 +1118,15 @@ int band_h2_groupwise_entry(const void* left, const void* right, float* out, int
 
 // Inner product / correlation fused with soft-argmin: disparity (N, H, W) fp32, and the volume
 // when out != nullptr.  fp32 features, one D pass (D <= 192); *handled = false otherwise.
+int64_t band_h2_fused_workspace_bytes(int64_t N, int64_t H, int64_t W, int64_t D) {
+  const int64_t npass = (std::max<int64_t>(D, 1) + 191) / 192;
+  return npass > 1 ? npass * N * H * W * (8 + 8 + 4) : 0;
+}
+
 int band_h2_fused_entry(const void* left, const void* right, void* out, float* disp, int dtype,
                         int64_t N, int64_t C, int64_t H, int64_t W, int64_t D,
                         const int64_t* l_strides, const int64_t* r_strides, int mode,
-                        void* stream, bool* handled) {
+                        void* stream, bool* handled, void* workspace, int64_t ws_bytes) {
   using namespace h2band;
   *handled = false;
   if (disp == nullptr && N * H * W > 0) return fail(SM_EINVAL, "null disparity pointer");
@@ -1095,7 +1141,17 @@ int band_h2_fused_entry(const void* left, const void* right, void* out, float* d
     return SM_OK;
   }
   vec = vec && reinterpret_cast<uintptr_t>(disp) % 16 == 0;
-  if (!vec || dtype != SM_F32 || a.npass != 1 || D == 0) return SM_OK;
+  // D > 192 (several passes): volume-free only, with a workspace for the partial states
+  const bool multi = a.npass > 1 && out == nullptr && workspace != nullptr &&
+                     ws_bytes >= band_h2_fused_workspace_bytes(N, H, W, D) &&
+                     reinterpret_cast<uintptr_t>(workspace) % 8 == 0;
+  if (!vec || dtype != SM_F32 || (a.npass != 1 && !multi) || D == 0) return SM_OK;
+  if (multi) {
+    const int64_t per = (int64_t)a.npass * a.nhw;
+    a.ws_s = static_cast<double*>(workspace);
+    a.ws_t = a.ws_s + per;
+    a.ws_m = reinterpret_cast<float*>(a.ws_t + per);
+  }
   *handled = true;
   a.out = out;
   a.disp = disp;
@@ -1109,8 +1165,12 @@ int band_h2_fused_entry(const void* left, const void* right, void* out, float* d
     if (out != nullptr)
       return mean ? launch<float, float, TM, true, h2band::kNDHW, 1>(a, N, st)
                   : launch<float, float, TM, false, h2band::kNDHW, 1>(a, N, st);
-    return mean ? launch<float, float, TM, true, h2band::kNDHW, 2>(a, N, st)
-                : launch<float, float, TM, false, h2band::kNDHW, 2>(a, N, st);
+    const int rc = mean ? launch<float, float, TM, true, h2band::kNDHW, 2>(a, N, st)
+                        : launch<float, float, TM, false, h2band::kNDHW, 2>(a, N, st);
+    if (rc != SM_OK || a.ws_m == nullptr) return rc;
+    hipLaunchKernelGGL(fused_merge_kernel, dim3((unsigned)ceil_div(a.nhw, (int64_t)256)), dim3(256), 0,
+                       st, a.ws_s, a.ws_t, a.ws_m, a.npass, a.nhw, disp);
+    return check_launch("fused_merge_kernel");
   });
 }
 

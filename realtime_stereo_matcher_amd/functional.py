@@ -169,8 +169,10 @@ def inner_product_soft_argmin(left, right, max_disparity, mean=False, keep_volum
     sum_d d * softmax_d(volume) (model/mobile_disp_net_c.py:208-220, = the inline soft-argmin of
     model/mobile_stereo_net.py:144-147).  Returns ``(volume, disparity)``: the (N,D,H,W) volume
     (``None`` with ``keep_volume=False``: it is then never written) and the (N,1,H,W) disparity,
-    both in the feature dtype.  fp32 features with W % 4 == 0 and D <= 192 run one fused band
-    kernel; other shapes run the volume and the regression kernels back to back.
+    both in the feature dtype.  fp32 features (W >= 4) run one fused band kernel for D <= 192;
+    without the volume also for D > 192 (passes of <= 192 disparities whose partial softmax
+    states a second kernel merges, in a workspace allocated here); other shapes run the volume
+    and the regression kernels back to back.
     """
     left, right, dev, code = _pair(left, right, "inner_product_soft_argmin")
     D = _disp(max_disparity, "inner_product_soft_argmin")
@@ -178,9 +180,13 @@ def inner_product_soft_argmin(left, right, max_disparity, mean=False, keep_volum
     mode = 1 if mean else 0
 
     def call(vol, disp):
-        return _lib.load().sm_cv_inner_product_softargmin(
+        lib = _lib.load()
+        nws = int(lib.sm_cv_inner_product_softargmin_workspace_bytes(n, h, w, D)) if vol is None else 0
+        ws = torch.empty(nws, dtype=torch.uint8, device=dev) if nws > 0 else None
+        return lib.sm_cv_inner_product_softargmin_ws(
             _ptr(left), _ptr(right), None if vol is None else _ptr(vol), _ptr(disp), code,
-            n, c, h, w, D, _lib.strides_arg(left), _lib.strides_arg(right), mode, _stream(dev))
+            n, c, h, w, D, _lib.strides_arg(left), _lib.strides_arg(right), mode,
+            None if ws is None else _ptr(ws), nws, _stream(dev))
 
     def fn(keep):
         vol = torch.empty((n, D, h, w), dtype=left.dtype, device=dev) if keep else None
