@@ -58,6 +58,10 @@ def main():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     dst_root = os.path.join(root, "profiles", rnd)
     summary = {}
+    spath = os.path.join(dst_root, "summary.json")
+    if os.path.exists(spath):  # several evidence runs fold into one summary (rows replaced by name)
+        with open(spath) as f:
+            summary = json.load(f)
     for d in sorted(glob.glob(os.path.join(src, "*"))):
         if not os.path.isdir(d) or not os.path.exists(os.path.join(d, "bench.json")):
             continue
