@@ -50,7 +50,7 @@ int main(int argc, char** argv) {
     if (h2) return smcv::band_h2_entry(L, R, O, SM_F32, N, C, H, W, D, nullptr, nullptr, 0, nullptr, &handled);
     if (fused || fusednv)
       return smcv::band_h2_fused_entry(L, R, fused ? O : nullptr, disp, SM_F32, N, C, H, W, D, nullptr,
-                                       nullptr, 0, nullptr, &handled);
+                                       nullptr, 0, nullptr, &handled, nullptr, 0);
     if (gw)
       return smcv::band_h2_groupwise_entry(L, R, O, SM_BF16, N, C, H, W, D, G, nullptr, nullptr, nullptr,
                                            &handled);

@@ -50,7 +50,7 @@ int main(int argc, char** argv) {
     if (!strcmp(mode, "h2") || x8) return smcv::band_h2_entry(L, R, O, SM_F32, N, C, H, W, D, nullptr, nullptr, 0, nullptr, &handled);
     if (!strcmp(mode, "h2fused") || !strcmp(mode, "h2fusednv"))
       return smcv::band_h2_fused_entry(L, R, !strcmp(mode, "h2fused") ? O : nullptr, disp, SM_F32, N, C, H, W, D,
-                                       nullptr, nullptr, 0, nullptr, &handled);
+                                       nullptr, nullptr, 0, nullptr, &handled, nullptr, 0);
     if (!strcmp(mode, "wsfused") || !strcmp(mode, "wsfusednv"))
       return smcv::band_ws_fused_entry(L, R, !strcmp(mode, "wsfused") ? O : nullptr, disp, SM_F32, N, C, H, W, D,
                                        nullptr, nullptr, 0, nullptr, &handled);
