@@ -125,3 +125,13 @@ def test_product_package_never_imports_oracle():
             if f.endswith(".py"):
                 src = open(os.path.join(dirpath, f)).read()
                 assert "oracle" not in re.sub(r'""".*?"""', "", src, flags=re.S), f
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    """No CPU fallback: without the shared object every operator raises ImportError."""
+    from realtime_stereo_matcher_amd import _lib
+
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "libstereocv.so"))
+    with pytest.raises(ImportError, match="no CPU fallback|There is no CPU fallback"):
+        _lib.load()
