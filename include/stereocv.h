@@ -99,8 +99,8 @@ int sm_cv_inner_product_softargmin(const void* left, const void* right, void* ou
                                    int64_t W, int64_t D, const int64_t* l_strides,
                                    const int64_t* r_strides, int mode, void* stream);
 
-/* f-1 for D > 192 without the volume (e.g. make_correlation_volume + disparity_regression of
- * MobileDispNetC at D = 256, model/mobile_disp_net_c.py:188-220): the band kernel runs D in
+/* f-1 for D > 192 without the volume (e.g. make_correlation_volume followed by
+ * disparity_regression at D = 256, model/mobile_disp_net_c.py:188-220): the band kernel runs D in
  * passes of <= 192 disparities, each pass writes its partial softmax state per pixel into a
  * caller-provided device workspace (8-byte aligned, at least
  * sm_cv_inner_product_softargmin_workspace_bytes(N, H, W, D) bytes; 0 for D <= 192) and a
