@@ -666,6 +666,25 @@ def test_fused_soft_argmin_multipass(shape, mean):
     np.testing.assert_allclose(host(disp), host(disp2), atol=TOL, rtol=0)
 
 
+def test_cfg4_fused_volume_free_full_res():
+    """BASELINE configs[3] shape (1x16x1080x1920, correlation D = 256) through the volume-free
+    fused path (two passes + merge): the disparity matches the two-kernel pipeline's (volume,
+    then soft-argmin) within 1e-4 everywhere, and sampled rows match the fp64 soft-argmin of
+    the volume."""
+    from realtime_stereo_matcher_amd import functional as F
+
+    g = torch.Generator(device="cuda").manual_seed(3)
+    L = torch.randn(1, 16, 1080, 1920, device="cuda", generator=g)
+    R = torch.randn(1, 16, 1080, 1920, device="cuda", generator=g)
+    _, disp = F.inner_product_soft_argmin(L, R, 256, mean=True, keep_volume=False)
+    vol = F.correlation_volume(L, R, 256)
+    ref = F.soft_argmin(vol)
+    assert (disp - ref.view_as(disp)).abs().max().item() <= TOL
+    for y in (0, 540, 1079):
+        np.testing.assert_allclose(host(disp[:, :, y:y + 1]), O.softargmin(host(vol[:, :, y:y + 1])),
+                                   atol=TOL, rtol=0)
+
+
 def test_fused_soft_argmin_nonfinite_and_empty():
     from realtime_stereo_matcher_amd import functional as F
 
