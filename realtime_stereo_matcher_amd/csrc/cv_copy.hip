@@ -52,7 +52,8 @@ template <typename U, bool VEC, bool DV>
 __global__ __launch_bounds__(kThreads) void concat_kernel(const U* __restrict__ L,
                                                           const U* __restrict__ R,
                                                           U* __restrict__ out, int C, int H,
-                                                          int W, int D, Strides4 ls, Strides4 rs) {
+                                                          int W, int D, Strides4 ls, Strides4 rs,
+                                                          int lgdv) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_c[];
   U* Ls = reinterpret_cast<U*>(smem_c);
   U* Rs = Ls + W;
@@ -74,8 +75,9 @@ __global__ __launch_bounds__(kThreads) void concat_kernel(const U* __restrict__ 
       const unsigned e0 = v * NV;
       vec16<U> a, b;
       if (DV) {  // whole vector shares one x
-        const unsigned x = e0 / uD;
-        const unsigned d0 = e0 - x * uD;
+        // D / NV a power of two (lgdv >= 0, uniform): a shift instead of an integer division
+        const unsigned x = lgdv >= 0 ? v >> lgdv : e0 / uD;
+        const unsigned d0 = lgdv >= 0 ? (v & ((1u << lgdv) - 1)) * NV : e0 - x * uD;
         const U lx = Ls[x];
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
@@ -247,6 +249,8 @@ int concat_entry(const void* left, const void* right, void* out, int dtype, int6
   const int nv = 16 / es;
   const bool vec = ((W * D) % nv == 0) && aligned16(out);
   const bool dv = (D % nv == 0);
+  const int64_t dvec = D / nv;  // vectors per pixel on the DV path
+  const int lgdv = dv && (dvec & (dvec - 1)) == 0 ? __builtin_ctzll((unsigned long long)dvec) : -1;
   hipStream_t st = as_stream(stream);
   dim3 grid((unsigned)(N * C * H));
   const size_t shm = 2 * (size_t)W * es;
@@ -257,13 +261,13 @@ int concat_entry(const void* left, const void* right, void* out, int dtype, int6
     U* o = static_cast<U*>(out);                                                               \
     if (vec && dv)                                                                             \
       hipLaunchKernelGGL((concat_kernel<U, true, true>), grid, dim3(kThreads), shm, st, l, r, o, \
-                         (int)C, (int)H, (int)W, (int)D, ls, rs);                              \
+                         (int)C, (int)H, (int)W, (int)D, ls, rs, lgdv);                        \
     else if (vec)                                                                              \
       hipLaunchKernelGGL((concat_kernel<U, true, false>), grid, dim3(kThreads), shm, st, l, r, \
-                         o, (int)C, (int)H, (int)W, (int)D, ls, rs);                           \
+                         o, (int)C, (int)H, (int)W, (int)D, ls, rs, -1);                       \
     else                                                                                       \
       hipLaunchKernelGGL((concat_kernel<U, false, false>), grid, dim3(kThreads), shm, st, l, r, \
-                         o, (int)C, (int)H, (int)W, (int)D, ls, rs);                           \
+                         o, (int)C, (int)H, (int)W, (int)D, ls, rs, -1);                       \
   } while (0)
   if (es == 4) SM_CONCAT_LAUNCH(uint32_t); else SM_CONCAT_LAUNCH(uint16_t);
 #undef SM_CONCAT_LAUNCH
