@@ -860,10 +860,16 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
     SM_STAMP(2);
     __syncthreads();  // B: the planes of step s are complete
     SM_STAMP(0);
+    // the matrix phase at raised wave priority: while one workgroup feeds its MFMAs, the
+    // co-resident workgroup's staging / epilogue VALU yields issue slots to it (3-4 % faster on
+    // cfg2, profiles/r02/band_experiments/prio_mfma_phase.log; raising it in or outside the
+    // epilogue instead measured flat)
+    __builtin_amdgcn_s_setprio(1);
     if (ks == 0)
       band(std::true_type{});
     else
       band(std::false_type{});
+    __builtin_amdgcn_s_setprio(0);
     SM_STAMP(3);
     if (ks != nks - 1) return false;
     // ---- end of a segment: (fp32) range check, then the epilogue
