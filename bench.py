@@ -86,7 +86,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=None,
                     help="pairs per GPU per step (weak scaling; overrides --global-batch)")
     ap.add_argument("--chunk", type=int, default=None, help="pairs per kernel launch")
-    ap.add_argument("--algo", default="auto", choices=["auto", "h2", "ws", "bf16x3", "f32", "mfma", "valu"],
+    ap.add_argument("--algo", default="auto", choices=["auto", "h2", "bf16x3", "f32", "mfma", "valu"],
                     help="cfg2 volume kernel of --pipeline separate")
     ap.add_argument("--pipeline", default="separate",
                     choices=["separate", "fused", "fused-novolume", "interweave"])
@@ -127,7 +127,7 @@ def kernel_name(cfg, pipeline, algo):
         return "band_h2 (NGHWD, bf16)"
     if cfg["op"] == "inner_product" and pipeline == "separate":
         return {"valu": "dot_volume_valu", "f32": "ip_band_f32", "mfma": "ip_band_f32",
-                "bf16x3": "ip_band_mfma", "ws": "band_ws"}.get(algo, "band_h2")
+                "bf16x3": "ip_band_mfma"}.get(algo, "band_h2")
     return "band_h2 (fused soft-argmin)" if pipeline.startswith("fused") else "band_h2"
 
 
@@ -216,7 +216,7 @@ def check_numerics(cfg, a, L, R, last):
 
     lf = host(L[s0:s0 + 1].float())
     rf = host(R[s0:s0 + 1].float())
-    errs_v, errs_d, dev32, mean_d, mean32 = [], [], [], [], []
+    errs_v, errs_d, dev32, mean_d, mean32, vdev32 = [], [], [], [], [], []
     for y in rows:
         ly, ry = lf[:, :, y:y + 1], rf[:, :, y:y + 1]
         if cfg["op"] in ("inner_product", "correlation"):
@@ -225,8 +225,12 @@ def check_numerics(cfg, a, L, R, last):
             # the fp64 pipeline (exact volume, fp64 soft-argmin) and torch's fp32 pipeline on the
             # same rows: the fair bar for the end-to-end disparity
             exact = O.softargmin(ref).astype(np.float64)
-            t32 = soft_argmin_eager(sweep_dot_volume(torch.from_numpy(ly), torch.from_numpy(ry), D,
-                                                     mean=cfg["op"] == "correlation"))
+            v32 = sweep_dot_volume(torch.from_numpy(ly), torch.from_numpy(ry), D,
+                                   mean=cfg["op"] == "correlation")
+            # torch's own fp32 volume (the reference's op sequence) against the same fp64 rows:
+            # the fp32-rounding yardstick for max_abs_err_volume
+            vdev32.append(float(np.abs(v32.numpy().astype(np.float64) - ref).max()))
+            t32 = soft_argmin_eager(v32)
             d32 = np.abs(t32.numpy().astype(np.float64) - exact)
             dev32.append(float(d32.max()))
             mean32.append(float(d32.mean()))
@@ -248,6 +252,8 @@ def check_numerics(cfg, a, L, R, last):
             errs_v.append(0.0 if np.array_equal(got, ref) else float("inf"))
     if errs_v:
         out["max_abs_err_volume"] = max(errs_v)
+    if vdev32:
+        out["torch_fp32_volume_dev"] = max(vdev32)
     if errs_d:
         out["max_abs_err_disparity"] = max(errs_d)
     if dev32:

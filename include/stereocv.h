@@ -37,9 +37,12 @@ enum sm_status {
   SM_EUNSUPPORTED = -4 /* sm_cv_inner_product_softargmin without a volume: shape not fused */
 };
 enum sm_argext_mode { SM_ARGMIN = 0, SM_ARGMAX = 1 };
-enum sm_regress_flags {
+enum sm_regress_flags {         /* bit flags */
   SM_REGRESS_SOFTMAX = 0,      /* softmax over D inside (mobile_disp_net_c.py:208-220) */
-  SM_REGRESS_PRESOFTMAXED = 1  /* input already softmaxed (mobile_stereo_net_v4.py:10-14) */
+  SM_REGRESS_PRESOFTMAXED = 1, /* input already softmaxed (mobile_stereo_net_v4.py:10-14) */
+  SM_REGRESS_OUT_F32 = 2       /* fp32 output from an fp16 / bf16 volume: the reference's autocast
+                                  eval, where F.softmax and torch.sum run in fp32
+                                  (mobile_stereo_net.py:144-147 under evaluate_stereo.py:48) */
 };
 /* Inner-product kernel selection (sm_cv_inner_product_ex). */
 enum sm_ip_algo {
@@ -48,14 +51,9 @@ enum sm_ip_algo {
   SM_IP_MFMA_F32 = 2,    /* banded C-contraction on v_mfma_f32_16x16x4_f32 (exact fp32 fma) */
   SM_IP_MFMA_BF16X3 = 3, /* banded C-contraction on bf16 MFMA over an exact 3-way bf16 split */
   /* 4: reserved (a retired warp-specialised variant of the bf16 split) */
-  SM_IP_MFMA_H2 = 5,     /* banded contraction on 32x32x16 MFMA, two workgroups per CU, every wave
+  SM_IP_MFMA_H2 = 5      /* banded contraction on 32x32x16 MFMA, two workgroups per CU, every wave
                             loads, stages, multiplies and stores (the default) */
-  SM_IP_MFMA_WS = 6      /* the same banded contraction, one warp-specialised workgroup
-                            per CU: 4 staging waves (loads, operand conversion) feed 4 MFMA
-                            waves (matrix work, shear, stores) through two LDS stage slots.
-                            fp16 / bf16 features as they are (exact products), fp32 features as
-                            a per-item power-of-two scaled, range-checked two-plane fp16 split
-                            rounded to nearest (items holding +-inf take an exact fp32 path) */
+  /* 6: reserved (a retired warp-specialised variant, removed in round 3) */
 };
 
 /* Library version (major*10000 + minor*100 + patch). */
@@ -155,7 +153,8 @@ int sm_cv_diff(const void* left, const void* right, void* out, int dtype,
  *   flags = SM_REGRESS_SOFTMAX:      sum_d d * softmax_d(v)   (mobile_disp_net_c.py:208-220,
  *                                    inline mobile_stereo_net.py:144-147)
  *   flags = SM_REGRESS_PRESOFTMAXED: sum_d d * v              (mobile_stereo_net_v4.py:10-14)
- * out: (N, H, W) in `dtype` (keepdim is a caller-side view).  fp64 accumulation.
+ * out: (N, H, W) in `dtype` (keepdim is a caller-side view), or float32 with
+ * SM_REGRESS_OUT_F32 (flags may OR it with either mode).  fp64 accumulation.
  * vol_strides: element strides of (N, D, H, W), W stride must be 1 (NULL = contiguous).
  * Any 4-byte aligned out works; fp32 planes with a 16-B aligned volume AND out take the
  * vectorised one-wave kernel, other alignments the generic kernel (same results). */

@@ -86,3 +86,61 @@ def sweep_interweave_shifted(left, right, num_disp):
         vol[:, 0::2, shift, :, shift:] = left[..., shift:]
         vol[:, 1::2, shift, :, shift:] = right[..., : w - shift]
     return vol
+
+
+# ---------------------------------------------------------------- eager restatements for the
+# model-level isolation test (tests/test_model_isolation.py): the same networks run once with the
+# engine's ops and once with these, on the same device and the same MIOpen trunk, so the
+# difference is the engine's own contribution.  Device-agnostic torch code.
+def sweep_diff_volume(left, right, num_disp):
+    """make_cost_volume (model/mobile_stereo_net.py:8-27): L - R(x-d) at x >= d, 1.0 elsewhere,
+    (N, C, D, H, W) in the left dtype."""
+    n, c, h, w = left.shape
+    vol = left.new_ones((n, c, num_disp, h, w))
+    for shift in range(min(num_disp, w)):
+        vol[:, :, shift, :, shift:] = left[..., shift:] - right[..., : w - shift]
+    return vol
+
+
+def soft_argmin_fp64(volume, keepdim=True):
+    """The reference's softmax-then-weighted-sum over D (mobile_stereo_net.py:144-147) evaluated in
+    fp64 and rounded once to fp32: the exact regression of the given volume."""
+    v = volume.double()
+    p = F.softmax(v, dim=1)
+    d = torch.arange(v.shape[1], dtype=torch.float64, device=v.device).view(1, -1, 1, 1)
+    return (p * d).sum(dim=1, keepdim=keepdim).float()
+
+
+def regression_presoftmax_fp64(x, maxdisp):
+    """mobile_stereo_net_v4.py:10-14 in fp64, rounded once to fp32."""
+    d = torch.arange(maxdisp, dtype=torch.float64, device=x.device).view(1, maxdisp, 1, 1)
+    return (x.double() * d).sum(dim=1).float()
+
+
+def warp_grid_sample(image, flow):
+    """tools/warp.py:5-42 restated: grid (x - fx, y - fy) normalised by (w - 1, h - 1), then
+    F.grid_sample bilinear, zero padding, align_corners=False."""
+    n, c, h, w = flow.shape
+    gy, gx = torch.meshgrid(torch.arange(h, device=image.device, dtype=image.dtype),
+                            torch.arange(w, device=image.device, dtype=image.dtype), indexing="ij")
+    gx = (gx.view(1, 1, h, w) - flow[:, 0:1]).permute(0, 2, 3, 1)
+    if c == 2:
+        gy = (gy.view(1, 1, h, w) - flow[:, 1:2]).permute(0, 2, 3, 1)
+    else:
+        gy = gy.view(1, h, w, 1).expand(n, h, w, 1)
+    grid = torch.cat((2.0 * gx / (w - 1.0) - 1.0, 2.0 * gy / (h - 1.0) - 1.0), dim=-1)
+    return F.grid_sample(image, grid, mode="bilinear", padding_mode="zeros", align_corners=False)
+
+
+def v4_volume_loop(featL, featR, conv3d, volume11, volume_size):
+    """MobileStereoNetV4's per-disparity loop (model/mobile_stereo_net_v4.py:443-461): interleave
+    L[..., i:] (even channels) and R[..., :-i] (odd), run the Conv3d stack and volume11 on the
+    crop, place the result at x >= i of a zero (N, D, H, W) volume."""
+    b, c, h, w = featL.shape
+    vol = featL.new_zeros((b, volume_size, h, w))
+    for i in range(min(volume_size, w)):
+        lx, rx = featL[..., i:], featR[..., : w - i]
+        x = torch.stack((lx, rx), dim=2).reshape(b, 2 * c, h, w - i)
+        x = volume11(conv3d(x.unsqueeze(1)).squeeze(2))
+        vol[:, i, :, i:] = x[:, 0]
+    return vol

@@ -30,20 +30,6 @@ int v4_volume_entry(const float* L, const float* R, float* out, int64_t N, int64
                     const float* w1, const float* b1, const float* w2, const float* b2,
                     const float* w3, const float* b3, const float* w4, const float* b4,
                     void* workspace, size_t workspace_bytes, hipStream_t st);
-int band_ws_entry(const void* left, const void* right, void* out, int dtype, int64_t N, int64_t C,
-                  int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
-                  const int64_t* r_strides, int mode, void* stream, bool* handled);
-int band_ws_groupwise_entry(const void* left, const void* right, float* out, int dtype, int64_t N,
-                            int64_t C, int64_t H, int64_t W, int64_t D, int64_t G,
-                            const int64_t* l_strides, const int64_t* r_strides, void* stream,
-                            bool* handled);
-int band_ws_fused_entry(const void* left, const void* right, void* out, float* disp, int dtype,
-                        int64_t N, int64_t C, int64_t H, int64_t W, int64_t D,
-                        const int64_t* l_strides, const int64_t* r_strides, int mode,
-                        void* stream, bool* handled);
-int ip_mfma_entry(const void* left, const void* right, void* out, int dtype, int64_t N,
-                  int64_t C, int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
-                  const int64_t* r_strides, void* stream, bool* handled);
 int concat_entry(const void* left, const void* right, void* out, int dtype, int64_t N,
                  int64_t C, int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
                  const int64_t* r_strides, void* stream);
@@ -77,14 +63,6 @@ extern "C" int sm_cv_inner_product_ex(const void* left, const void* right, void*
       bool handled = false;
       int rc = band_f32_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
                               stream, &handled);
-      if (handled || rc != SM_OK) return rc;
-      return dot_volume_valu_entry(left, right, out, dtype, N, C, H, W, D, 1, l_strides,
-                                   r_strides, 0, stream);
-    }
-    case SM_IP_MFMA_WS: {  // the warp-specialised band kernel; odd shapes: the exact VALU kernel
-      bool handled = false;
-      int rc = band_ws_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
-                             stream, &handled);
       if (handled || rc != SM_OK) return rc;
       return dot_volume_valu_entry(left, right, out, dtype, N, C, H, W, D, 1, l_strides,
                                    r_strides, 0, stream);

@@ -274,9 +274,10 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
   using G = Geo<T, TMAX>;
   constexpr int DMAX = G::DMAX;
   constexpr int NP = G::NP;
-  // The fused kernels run one workgroup per CU with the accumulators partly in AGPRs, where the
-  // register allocator splits live ranges with copies: hand-counted asm loads (and L2 touches)
-  // are not safe there, so they use compiler-tracked loads.
+  // Every instantiation (the fused ones too) runs two workgroups per CU with hand-counted asm
+  // feature loads: vm_wait names how many younger vector-memory operations may stay in flight
+  // after a segment -- 4 (T-1) volume stores (+1 disparity store for FUSE 1), one disparity
+  // store for FUSE 2 -- and scripts/check_h2_asm.py verifies the count on the compiled asm.
   constexpr bool ASM = true;
   constexpr int PF = ASM ? kPF : 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -794,10 +795,10 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
         const int x = k.x0 + xx;
         if (x >= W) continue;
         float m = -INFINITY;
-        double s = 0.0, t = 0.0;
+        double s = 0.0, t = 0.0;  // relative to m; t over the pass-local d
         bool nan = false;
         for (int d = 0; d < k.Dp; ++d) {
-          const float v = cell(x, d);
+          const float v = cell(x, k.dp + d);
           nan |= v != v;
           if (v > m) {
             const double f = m == -INFINITY ? 0.0 : (double)expf(m - v);
@@ -811,8 +812,22 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
             t += (double)d * e;
           }
         }
-        store_one<float>(args.disp + ((size_t)k.n * H + k.y) * W + x,
-                         (nan || m == INFINITY || m == -INFINITY) ? NAN : (float)(t / s));
+        const size_t px = ((size_t)k.n * H + k.y) * W + x;
+        if (args.ws_m != nullptr) {
+          // one of several D passes: the same partial state as fuse_regs (d global); a NaN cell or
+          // a +inf maximum is carried as s = NaN, which fused_merge_kernel propagates; an all -inf
+          // pass (s = 0, m = -inf) contributes nothing, and all -inf passes give 0 / 0 = NaN
+          typedef __attribute__((address_space(1))) void gvoid;
+          const size_t o = (size_t)k.pass * ((size_t)args.nhw) + px;
+          const double sv = (nan || m == INFINITY) ? (double)NAN : s;
+          *reinterpret_cast<__attribute__((address_space(1))) double*>((gvoid*)(args.ws_s + o)) = sv;
+          *reinterpret_cast<__attribute__((address_space(1))) double*>((gvoid*)(args.ws_t + o)) =
+              t + (double)k.dp * sv;
+          store_one<float>(args.ws_m + o, m);
+        } else {
+          store_one<float>(args.disp + px,
+                           (nan || m == INFINITY || m == -INFINITY) ? NAN : (float)(t / s));
+        }
       }
     }
   };
@@ -1166,8 +1181,8 @@ int band_h2_fused_entry(const void* left, const void* right, void* out, float* d
   hipStream_t st = as_stream(stream);
   return by_tmax(a.pw, [&](auto tm) {
     constexpr int TM = decltype(tm)::value;
-    // FUSE 1: volume + disparities (one workgroup per CU, 512 registers); FUSE 2: disparities
-    // only -- no shear, no ring, no volume stores, two workgroups per CU
+    // FUSE 1: volume + disparities; FUSE 2: disparities only -- no shear, no ring, no volume
+    // stores.  Both two workgroups per CU with hand-counted loads (see band_h2).
     if (out != nullptr)
       return mean ? launch<float, float, TM, true, h2band::kNDHW, 1>(a, N, st)
                   : launch<float, float, TM, false, h2band::kNDHW, 1>(a, N, st);

@@ -632,11 +632,4 @@ int band_mfma_entry(const void* left, const void* right, void* out, int dtype, i
   }
 }
 
-int ip_mfma_entry(const void* left, const void* right, void* out, int dtype, int64_t N, int64_t C,
-                  int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
-                  const int64_t* r_strides, void* stream, bool* handled) {
-  *handled = true;
-  return band_mfma_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0, stream);
-}
-
 }  // namespace smcv

@@ -31,9 +31,12 @@ struct VolView {
 // [w*Dq, (w+1)*Dq).  Each lane keeps an online softmax (running max m, fp64 sums s = sum e,
 // t = sum d*e) per pixel; the four partial states are merged through LDS by wave 0.  Splitting
 // D across waves gives 4x the loads in flight of a one-wave-per-pixel sweep.
-template <typename T, int PX, bool PRESOFT>
+// TO: the output dtype -- T, or float for an fp16 / bf16 volume regressed to fp32 (the
+// reference's autocast eval: F.softmax and torch.sum run in fp32 on an fp16 volume,
+// mobile_stereo_net.py:144-147 under evaluate_stereo.py:48).
+template <typename T, typename TO, int PX, bool PRESOFT>
 __global__ __launch_bounds__(kThreads) void softargmin_kernel(const T* __restrict__ vol,
-                                                              T* __restrict__ out, int D, int H,
+                                                              TO* __restrict__ out, int D, int H,
                                                               int W, VolView vs) {
   __shared__ float sm_m[4][PX][64];
   __shared__ double sm_s[4][PX][64];
@@ -137,7 +140,7 @@ __global__ __launch_bounds__(kThreads) void softargmin_kernel(const T* __restric
   }
   __syncthreads();
   if (wave != 0 || !any) return;
-  T* o = out + ((int64_t)n * H + y) * W + x0;
+  TO* o = out + ((int64_t)n * H + y) * W + x0;
 #pragma unroll
   for (int p = 0; p < PX; ++p) {
     if (x0 + p >= W) continue;
@@ -168,7 +171,7 @@ __global__ __launch_bounds__(kThreads) void softargmin_kernel(const T* __restric
       // NaN anywhere in the column, or an all -inf / any +inf column, gives NaN as in torch
       r = (nan || M == INFINITY || M == -INFINITY) ? NAN : (float)(Tt / S);
     }
-    o[p] = from_f<T>(r);
+    o[p] = from_f<TO>(r);
   }
 }
 
@@ -424,11 +427,13 @@ int softargmin_entry(const void* volume, void* out, int dtype, int64_t N, int64_
   VolView vs;
   int rc = check_vol(volume, out, dtype, N, D, H, W, vol_strides, &vs);
   if (rc) return rc;
-  if (flags != SM_REGRESS_SOFTMAX && flags != SM_REGRESS_PRESOFTMAXED)
+  if ((flags & ~(SM_REGRESS_PRESOFTMAXED | SM_REGRESS_OUT_F32)) != 0)
     return fail(SM_EINVAL, "unknown regression flags");
   if (N * H * W == 0) return SM_OK;
   hipStream_t st = as_stream(stream);
-  const bool presoft = flags == SM_REGRESS_PRESOFTMAXED;
+  const bool presoft = (flags & SM_REGRESS_PRESOFTMAXED) != 0;
+  // fp32 output from an fp16 / bf16 volume (for an fp32 volume the flag changes nothing)
+  const bool out32 = (flags & SM_REGRESS_OUT_F32) != 0 && dtype != SM_F32;
   flatten_plane(vs, &H, &W);
   const bool flat4 = dtype == SM_F32 && (H == 1) && (W % 4 == 0) &&
                      (vs.d % 4 == 0) && (vs.n % 4 == 0) && (H * W < (int64_t)1 << 30) &&
@@ -451,26 +456,34 @@ int softargmin_entry(const void* volume, void* out, int dtype, int64_t N, int64_
   }
   const bool v4 = dtype == SM_F32 && (W % 4 == 0) && (vs.h % 4 == 0) && (vs.d % 4 == 0) &&
                   (vs.n % 4 == 0) && ((reinterpret_cast<uintptr_t>(volume) & 15u) == 0);
-  SM_DISPATCH_DTYPE(dtype, T, {
+  auto go = [&](auto tin, auto tout) {
+    using T = decltype(tin);
+    using TO = decltype(tout);
     const T* v = static_cast<const T*>(volume);
-    T* o = static_cast<T*>(out);
+    TO* o = static_cast<TO*>(out);
     if (v4) {
       dim3 grid((unsigned)ceil_div(W, 64 * 4), (unsigned)H, (unsigned)N);
       if (presoft)
-        hipLaunchKernelGGL((softargmin_kernel<T, 4, true>), grid, dim3(kThreads), 0, st, v, o,
+        hipLaunchKernelGGL((softargmin_kernel<T, TO, 4, true>), grid, dim3(kThreads), 0, st, v, o,
                            (int)D, (int)H, (int)W, vs);
       else
-        hipLaunchKernelGGL((softargmin_kernel<T, 4, false>), grid, dim3(kThreads), 0, st, v, o,
+        hipLaunchKernelGGL((softargmin_kernel<T, TO, 4, false>), grid, dim3(kThreads), 0, st, v, o,
                            (int)D, (int)H, (int)W, vs);
     } else {
       dim3 grid((unsigned)ceil_div(W, 64), (unsigned)H, (unsigned)N);
       if (presoft)
-        hipLaunchKernelGGL((softargmin_kernel<T, 1, true>), grid, dim3(kThreads), 0, st, v, o,
+        hipLaunchKernelGGL((softargmin_kernel<T, TO, 1, true>), grid, dim3(kThreads), 0, st, v, o,
                            (int)D, (int)H, (int)W, vs);
       else
-        hipLaunchKernelGGL((softargmin_kernel<T, 1, false>), grid, dim3(kThreads), 0, st, v, o,
+        hipLaunchKernelGGL((softargmin_kernel<T, TO, 1, false>), grid, dim3(kThreads), 0, st, v, o,
                            (int)D, (int)H, (int)W, vs);
     }
+  };
+  SM_DISPATCH_DTYPE(dtype, T, {
+    if (out32)
+      go(T{}, float{});
+    else
+      go(T{}, T{});
   });
   return check_launch("softargmin_kernel");
 }

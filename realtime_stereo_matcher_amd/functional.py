@@ -29,7 +29,7 @@ from . import _lib
 _DTYPES = {torch.float32: _lib.SM_F32, torch.float16: _lib.SM_F16, torch.bfloat16: _lib.SM_BF16}
 _ALGOS = {"auto": _lib.SM_IP_AUTO, "valu": _lib.SM_IP_VALU, "mfma": _lib.SM_IP_MFMA_F32,
           "f32": _lib.SM_IP_MFMA_F32, "bf16x3": _lib.SM_IP_MFMA_BF16X3,
-          "h2": _lib.SM_IP_MFMA_H2, "ws": _lib.SM_IP_MFMA_WS}
+          "h2": _lib.SM_IP_MFMA_H2}
 
 
 # ----------------------------------------------------------------------------------- plumbing
@@ -120,6 +120,23 @@ def _ptr(t):
     return t.data_ptr()
 
 
+_HALF = (torch.float16, torch.bfloat16)
+
+
+def _autocast_fp32(*ts):
+    """True when torch autocast is active on the tensors' device and one of them is fp16 / bf16.
+
+    The reference evaluates under ``torch.cuda.amp.autocast`` (``mixed_precision`` defaults to
+    True: evaluate_stereo.py:48,124,182,231,320; test_stereo.py:117).  Its Conv3d outputs are
+    then fp16, but ``F.softmax``, ``torch.sum`` and ``F.grid_sample`` are autocast fp32 ops, so
+    the soft-argmin (mobile_stereo_net.py:144-147, mobile_disp_net_c.py:208-220) returns an fp32
+    disparity from an fp16 volume and the RefineNet warp (tools/warp.py:39) samples in fp32.
+    The engine follows: under autocast these ops return fp32 (one rounding, from fp64 / fp32
+    arithmetic), never the volume's reduced dtype.
+    """
+    return any(t.dtype in _HALF for t in ts) and torch.is_autocast_enabled(ts[0].device.type)
+
+
 # ----------------------------------------------------------------------------- a-1, a-6, a-2
 def inner_product_volume(left, right, max_disparity, algo="auto"):
     """(N,C,H,W) x2 -> (N,D,H,W): sum_c L*R(x-d) for x >= d, 0 elsewhere (left dtype/device)."""
@@ -178,10 +195,19 @@ def inner_product_soft_argmin(left, right, max_disparity, mean=False, keep_volum
     D = _disp(max_disparity, "inner_product_soft_argmin")
     n, c, h, w = left.shape
     mode = 1 if mean else 0
+    if _autocast_fp32(left):
+        # autocast eval with fp16 / bf16 features: the volume keeps the feature dtype (the
+        # reference assigns into zeros of left.dtype) and the soft-argmin returns fp32; the fused
+        # kernel takes fp32 features only, so this is the two-kernel path either way
+        vol = correlation_volume(left, right, D) if mean else inner_product_volume(left, right, D)
+        return (vol if keep_volume else None), soft_argmin(vol)
 
     def call(vol, disp):
         lib = _lib.load()
-        nws = int(lib.sm_cv_inner_product_softargmin_workspace_bytes(n, h, w, D)) if vol is None else 0
+        # the workspace serves only the volume-free fused kernel over several D passes, which
+        # takes fp32 features; other dtypes fall back to the two-kernel path without it
+        nws = (int(lib.sm_cv_inner_product_softargmin_workspace_bytes(n, h, w, D))
+               if vol is None and code == _lib.SM_F32 else 0)
         ws = torch.empty(nws, dtype=torch.uint8, device=dev) if nws > 0 else None
         return lib.sm_cv_inner_product_softargmin_ws(
             _ptr(left), _ptr(right), None if vol is None else _ptr(vol), _ptr(disp), code,
@@ -350,9 +376,13 @@ def _volume(volume, what):
 def _regress(volume, flags, what):
     vol, dev, code = _volume(volume, what)
     n, d, h, w = vol.shape
+    odt = vol.dtype
+    if _autocast_fp32(vol):  # autocast: F.softmax / torch.sum run in fp32 (see _autocast_fp32)
+        flags |= _lib.SM_REGRESS_OUT_F32
+        odt = torch.float32
 
     def fn():
-        out = torch.empty((n, h, w), dtype=vol.dtype, device=dev)
+        out = torch.empty((n, h, w), dtype=odt, device=dev)
         if out.numel():
             lib = _lib.load()
             _lib.check(lib.sm_regress_softargmin(
@@ -364,13 +394,16 @@ def _regress(volume, flags, what):
 
 
 def soft_argmin(volume, keepdim=True):
-    """sum_d d * softmax_d(volume) -> (N,1,H,W) (keepdim) or (N,H,W); fp64 accumulation."""
+    """sum_d d * softmax_d(volume) -> (N,1,H,W) (keepdim) or (N,H,W); fp64 accumulation.
+    The output has the volume's dtype; under torch autocast an fp16 / bf16 volume gives fp32
+    (the reference's autocast F.softmax + torch.sum)."""
     out = _regress(volume, _lib.SM_REGRESS_SOFTMAX, "soft_argmin")
     return out.unsqueeze(1) if keepdim else out
 
 
 def regression_presoftmax(prob):
-    """sum_d d * prob[:, d] over an already-softmaxed (N,D,H,W) volume -> (N,H,W)."""
+    """sum_d d * prob[:, d] over an already-softmaxed (N,D,H,W) volume -> (N,H,W) (fp32 under
+    autocast for an fp16 / bf16 input, the reference's autocast torch.sum)."""
     return _regress(prob, _lib.SM_REGRESS_PRESOFTMAXED, "regression_presoftmax")
 
 
@@ -403,8 +436,14 @@ def warp_by_flow_map(image, flow):
 
     Mirrors ``warp_by_flow_map`` (tools/warp.py:5-42, model/mobile_stereo_net_v2.py:59-96,
     _v3.py:60-97): grid (x - fx, y - fy) normalised by (w - 1, h - 1), bilinear grid_sample with
-    zero padding and align_corners=False, evaluated by ONE HIP kernel (csrc/warp.hip).
-    float32 only; the same AssertionError as the reference for a flow with 3+ channels.
+    zero padding and align_corners=False, evaluated by ONE HIP kernel (csrc/warp.hip) in fp32;
+    the same AssertionError as the reference for a flow with 3+ channels.
+
+    Dtypes: float32 image and flow as they are.  fp16 / bf16 are read as fp32 and sampled in
+    fp32: under torch autocast (grid_sample is an autocast fp32 op, so the reference's RefineNet
+    warps an fp16 v3 feature map by an fp32 disparity and gets fp32) the output is fp32; without
+    autocast image and flow must share one dtype (as grid_sample requires) and the fp32 result is
+    rounded once to it.
     """
     if not isinstance(image, torch.Tensor) or not isinstance(flow, torch.Tensor):
         raise TypeError("warp_by_flow_map: image and flow must be tensors")
@@ -416,17 +455,28 @@ def warp_by_flow_map(image, flow):
         raise RuntimeError(f"warp_by_flow_map: expected a 4-D image, got {tuple(image.shape)}")
     if image.shape[0] != n:
         raise RuntimeError(f"warp_by_flow_map: image batch {image.shape[0]} != flow batch {n}")
-    if image.dtype != torch.float32 or flow.dtype != torch.float32:
-        raise TypeError(f"warp_by_flow_map: float32 image and flow only (got {image.dtype}, "
-                        f"{flow.dtype})")
+    for t in (image, flow):
+        if t.dtype not in _DTYPES:
+            raise TypeError(f"warp_by_flow_map: unsupported dtype {t.dtype}; expected float32, "
+                            "float16 or bfloat16")
     dev = _device_check(image, flow)
+    if _autocast_fp32(image, flow):
+        odt = torch.float32
+    elif image.dtype != flow.dtype:
+        raise RuntimeError(f"warp_by_flow_map: image ({image.dtype}) and flow ({flow.dtype}) must "
+                           "have the same dtype outside autocast (grid_sample's rule)")
+    else:
+        odt = image.dtype
+    # reduced-precision inputs are widened once on the device (exact); the kernel samples fp32
+    image = image.float() if image.dtype != torch.float32 else image
+    flow = flow.float() if flow.dtype != torch.float32 else flow
     image = _stride_ok(_rows_contiguous(image))
     flow = _stride_ok(_rows_contiguous(flow))
     N, C, Hi, Wi = image.shape
-    out = torch.empty((N, C, h, w), dtype=image.dtype, device=dev)
+    out = torch.empty((N, C, h, w), dtype=torch.float32, device=dev)
     if out.numel():
         lib = _lib.load()
         _lib.check(lib.sm_warp_by_flow(_ptr(image), _ptr(flow), _ptr(out), _lib.SM_F32, N, C, Hi,
                                        Wi, h, w, c, _lib.strides_arg(image),
                                        _lib.strides_arg(flow), _stream(dev)), "sm_warp_by_flow")
-    return out
+    return out if odt == torch.float32 else out.to(odt)

@@ -7,7 +7,6 @@
 #include "../realtime_stereo_matcher_amd/csrc/ip_mfma.hip"
 #include "../realtime_stereo_matcher_amd/csrc/ip_f32.hip"
 #include "../realtime_stereo_matcher_amd/csrc/ip_h2.hip"
-#include "../realtime_stereo_matcher_amd/csrc/ip_ws.hip"
 
 namespace smcv {
 __device__ unsigned long long g_stamps[4096][kStampPhases];
@@ -22,7 +21,7 @@ int main(int argc, char** argv) {
   // modes: bf16x3 (default), f32, h2 (inner product), fused (+ soft-argmin, volume kept),
   // fusednv (soft-argmin only), gw (groupwise bf16 cfg3: C=256, G=8, fp32 (N,G,H,W,D) out)
   const char* mode = argc > 2 ? argv[2] : "bf16x3";
-  const bool gw = !strcmp(mode, "gw") || !strcmp(mode, "wsgw");
+  const bool gw = !strcmp(mode, "gw");
   const int64_t N = 1, C = gw ? 256 : 64, H = 540, W = 960, D = argc > 1 ? atoi(argv[1]) : 192;
   const int64_t G = 8;
   const size_t nin = N * C * H * W, nout = gw ? N * G * H * W * D : N * D * H * W;
@@ -36,17 +35,9 @@ int main(int argc, char** argv) {
   const bool f32 = !strcmp(mode, "f32");
   const bool h2 = !strcmp(mode, "h2");
   const bool fused = !strcmp(mode, "fused"), fusednv = !strcmp(mode, "fusednv");
-  const bool ws = !strncmp(mode, "ws", 2);  // ws, wsfused, wsfusednv, wsgw
-  const bool band = h2 || fused || fusednv || gw || ws;
+  const bool band = h2 || fused || fusednv || gw;
   bool handled = false;
   auto run = [&]() {
-    if (!strcmp(mode, "ws")) return smcv::band_ws_entry(L, R, O, SM_F32, N, C, H, W, D, nullptr, nullptr, 0, nullptr, &handled);
-    if (!strcmp(mode, "wsfused") || !strcmp(mode, "wsfusednv"))
-      return smcv::band_ws_fused_entry(L, R, !strcmp(mode, "wsfused") ? O : nullptr, disp, SM_F32, N, C, H, W, D,
-                                       nullptr, nullptr, 0, nullptr, &handled);
-    if (!strcmp(mode, "wsgw"))
-      return smcv::band_ws_groupwise_entry(L, R, O, SM_BF16, N, C, H, W, D, G, nullptr, nullptr, nullptr,
-                                           &handled);
     if (h2) return smcv::band_h2_entry(L, R, O, SM_F32, N, C, H, W, D, nullptr, nullptr, 0, nullptr, &handled);
     if (fused || fusednv)
       return smcv::band_h2_fused_entry(L, R, fused ? O : nullptr, disp, SM_F32, N, C, H, W, D, nullptr,
@@ -92,27 +83,6 @@ int main(int argc, char** argv) {
   const char* names[12] = {"top barrier", "stage (split+lds)", "stage barrier", "mfma",
                            "epi barrier 1", "shear writes", "epi barrier 2", "store loop",
                            "stage: dma wait", "dma issue", "-", "-"};
-  if (ws) {  // per role: MFMA waves (phases 0-2) and staging waves (phases 3-6)
-    const char* wn[12] = {"M: barrier wait", "M: frags+mfma", "M: epilogue (+loop)", "P: barrier wait",
-                          "P: dma wait", "P: stage (ds_read, split, ds_write)", "P: dma issue (+loop)",
-                          "-", "-", "-", "-", "-"};
-    double sm[12] = {0};
-    int nm = 0, np = 0;
-    for (int w = 0; w < 4096; ++w) {
-      unsigned long long tm = st[w][0] + st[w][1] + st[w][2], tq = st[w][3] + st[w][4] + st[w][5] + st[w][6];
-      if (tm) ++nm;
-      if (tq) ++np;
-      for (int p = 0; p < 12; ++p) sm[p] += st[w][p];
-    }
-    const double tmw = (sm[0] + sm[1] + sm[2]) / (nm ? nm : 1), tpw = (sm[3] + sm[4] + sm[5] + sm[6]) / (np ? np : 1);
-    printf("kernel %s %.1f us rc=%d, MFMA waves %d (%.0f cycles/wave), staging waves %d (%.0f cycles/wave)\n", mode,
-           ms * 1e3, rc, nm, tmw, np, tpw);
-    for (int p = 0; p < 7; ++p) {
-      const double v = sm[p] / ((p < 3 ? nm : np) ? (p < 3 ? nm : np) : 1);
-      printf("  %-40s %10.0f cycles/wave  %5.1f %%\n", wn[p], v, 100.0 * v / (p < 3 ? tmw : tpw));
-    }
-    return 0;
-  }
   if (band) {
     const char* hn[12] = {"barrier waits", "wait+stage (split, lds write)", "load+touch issue",
                           "frags+mfma", "epilogue (shear, ring, stores)", "vm_wait step 0",

@@ -1,0 +1,113 @@
+"""The reference's default mixed-precision eval (VERDICT r02 "missing 1").
+
+The reference evaluates under ``torch.cuda.amp.autocast`` (``mixed_precision`` defaults to True:
+/root/reference/evaluate_stereo.py:48,124,182,231,320; test_stereo.py:117).  Conv3d outputs are
+then fp16, but F.softmax, torch.sum and F.grid_sample are autocast fp32 ops: the inline
+soft-argmin (model/mobile_stereo_net.py:144-147, _v2.py:217-220, _v3.py:321-324) and DispNetC's
+``disparity_regression`` (mobile_disp_net_c.py:208-220) return fp32 from an fp16 volume, and the
+RefineNet warp (tools/warp.py:39, called at mobile_stereo_net_v2.py:127 / _v3.py:136) samples an
+fp16 v3 feature map in fp32.  The engine must do the same -- fp32 out, from the fp16 values, within
+1e-4 of the fp64 regression -- and whole networks must run under autocast.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import stereo_oracle as O
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+def _vol(shape, scale, dt, seed=0):
+    v = np.random.default_rng(seed).standard_normal(shape).astype(np.float32) * scale
+    t = torch.from_numpy(v).cuda().to(dt)
+    return t, t.float().cpu().numpy()  # the exact fp16 / bf16 values, as fp32
+
+
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(1, 24, 60, 80), (2, 48, 7, 33), (1, 192, 3, 256)], ids=str)
+def test_soft_argmin_under_autocast_is_fp32(shape, dt):
+    from realtime_stereo_matcher_amd.model.mobile_disp_net_c import disparity_regression
+    from realtime_stereo_matcher_amd.model.mobile_stereo_net import soft_argmin_regression
+
+    V, v = _vol(shape, 4.0, dt)
+    want = O.softargmin(v)  # fp64 regression of the same (fp16 / bf16-representable) values
+    with torch.autocast("cuda", dtype=torch.float16):
+        outs = [soft_argmin_regression(V), disparity_regression(V, shape[1])]
+    for out in outs:
+        assert out.dtype == torch.float32 and out.shape == (shape[0], 1) + shape[2:]
+        np.testing.assert_allclose(out.cpu().numpy(), want, atol=TOL, rtol=0)
+    # outside autocast the reference keeps the volume's dtype (torch type rules)
+    assert soft_argmin_regression(V).dtype == dt
+
+
+def test_presoftmax_regression_under_autocast():
+    from realtime_stereo_matcher_amd.model.mobile_stereo_net_v4 import disparity_regression
+
+    p = torch.softmax(torch.randn(1, 48, 9, 40, device="cuda") * 3, dim=1).half()
+    with torch.autocast("cuda", dtype=torch.float16):
+        out = disparity_regression(p, 48)
+    assert out.dtype == torch.float32
+    want = O.regression_presoftmax(p.float().cpu().numpy(), 48)
+    np.testing.assert_allclose(out.cpu().numpy(), want, atol=TOL, rtol=0)
+
+
+def test_fused_call_under_autocast_fp16_features():
+    from realtime_stereo_matcher_amd import functional as F
+
+    l = torch.randn(1, 32, 4, 128, device="cuda").half()
+    r = torch.randn(1, 32, 4, 128, device="cuda").half()
+    with torch.autocast("cuda", dtype=torch.float16):
+        vol, disp = F.inner_product_soft_argmin(l, r, 48)
+        none, disp2 = F.inner_product_soft_argmin(l, r, 48, keep_volume=False)
+    assert vol.dtype == torch.float16 and disp.dtype == torch.float32 and none is None
+    np.testing.assert_allclose(disp.cpu().numpy(), O.softargmin(vol.float().cpu().numpy()), atol=TOL, rtol=0)
+    assert torch.equal(disp, disp2)
+
+
+def test_warp_under_autocast_fp16_feature_map_fp32_flow():
+    """v3 RefineNet: an fp16 feature map warped by the fp32 disparity -> fp32 (grid_sample is an
+    autocast fp32 op)."""
+    from realtime_stereo_matcher_amd.functional import warp_by_flow_map
+
+    g = torch.Generator(device="cuda").manual_seed(2)
+    img = torch.randn(1, 32, 30, 40, device="cuda", generator=g).half()
+    flow = torch.rand(1, 1, 30, 40, device="cuda", generator=g) * 20
+    with torch.autocast("cuda", dtype=torch.float16):
+        out = warp_by_flow_map(img, flow)
+        out2 = warp_by_flow_map(img, flow.half())  # both fp16 under autocast: fp32 too
+    assert out.dtype == torch.float32 and out2.dtype == torch.float32
+    want = O.warp_by_flow_map(img.float().cpu().numpy(), flow.cpu().numpy())
+    np.testing.assert_allclose(out.cpu().numpy(), want, atol=TOL, rtol=0)
+
+
+@pytest.mark.parametrize("v", ["v1", "v2", "v3", "dispnetc"])
+def test_networks_run_under_autocast(v):
+    """The demo networks under autocast: no dtype error anywhere (v2 / v3 warp the
+    fp32 disparity / an fp16 feature map), fp32 disparities out, and the same outputs as the
+    network with the eager reference restatements of the ops (oracle/torch_port.py) under the same
+    autocast, within fp16 convolution noise."""
+    from test_model_demo import _fixture, _net
+    from test_model_isolation import eager_ops
+
+    a = _fixture(v)
+    net = _net(a, v).cuda()
+    left, right = torch.from_numpy(a["left"]).cuda(), torch.from_numpy(a["right"]).cuda()
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.float16):
+        outs = net(left, right)
+        with eager_ops():
+            ref = net(left, right)
+    for o, r in zip(outs, ref):
+        assert o.dtype == r.dtype
+        assert torch.isfinite(o).all()
+        if v != "dispnetc":
+            assert o.dtype == torch.float32
+        err = (o.float() - r.float()).abs().max().item()
+        assert err <= 5e-2, err

@@ -482,8 +482,8 @@ def test_cfg2_inner_product_full_size(algo):
     from oracle.torch_port import soft_argmin_eager, sweep_dot_volume
 
     ln, rn = host(L), host(R)
-    rng = np.random.default_rng(3)
     worst = worst_torch = 0.0
+    mean_dev = []
     for y in (0, 1, 269, 538, 539):
         ref = O.inner_product(ln[:, :, y:y + 1], rn[:, :, y:y + 1], 192)
         got_v = host(vol[:, :, y:y + 1])
@@ -494,20 +494,23 @@ def test_cfg2_inner_product_full_size(algo):
         # end to end, per pixel: |disp - fp64 pipeline| against the same deviation of torch's
         # own fp32 pipeline (the reference's arithmetic) on these rows.  fp32-volume rounding is
         # amplified by sharp / bimodal softmaxes at a few pixels, for torch as for the kernel
-        # (same amplification, different rounding), so the bar is max(1e-4, 2x the torch-fp32
-        # deviation) over the sampled rows; the EPE against any ground truth then differs from
-        # the exact pipeline's by at most that.
+        # (same amplification, different rounding).  Two bars, both written here:
+        #   EPE level (north star "EPE identical within 1e-4"): the MEAN per-pixel |disp - fp64
+        #     pipeline| over the sampled rows <= 1e-4 -- it bounds |EPE_kernel - EPE_exact| for
+        #     ANY ground truth;
+        #   per pixel (a relaxation of 1e-4, stated in DESIGN §4): max |disp - fp64 pipeline|
+        #     <= max(1e-4, 2 x torch fp32's own per-pixel deviation on the same rows).
         exact = O.softargmin(ref).astype(np.float64)
         t32 = soft_argmin_eager(sweep_dot_volume(torch.from_numpy(ln[:, :, y:y + 1]),
                                                  torch.from_numpy(rn[:, :, y:y + 1]), 192))
         worst_torch = max(worst_torch, np.abs(t32.numpy().astype(np.float64) - exact).max())
-        worst = max(worst, np.abs(got_d.astype(np.float64) - exact).max())
-        gt = rng.uniform(0, 191, size=got_d.shape)
-        epe_kernel = np.abs(got_d - gt).mean()
-        epe_exact = np.abs(exact - gt).mean()
-        assert abs(epe_kernel - epe_exact) <= TOL, (epe_kernel, epe_exact)
-    print(f"cfg2 {algo}: max per-pixel |disp - fp64 pipeline|: kernel {worst:.3g}, "
-          f"torch fp32 {worst_torch:.3g}")
+        dd = np.abs(got_d.astype(np.float64) - exact)
+        worst = max(worst, dd.max())
+        mean_dev.append(dd.mean())
+    mean_abs = float(np.mean(mean_dev))
+    print(f"cfg2 {algo}: per-pixel |disp - fp64 pipeline|: max kernel {worst:.3g}, "
+          f"torch fp32 {worst_torch:.3g}; mean kernel {mean_abs:.3g}")
+    assert mean_abs <= TOL, mean_abs
     assert worst <= max(TOL, 2 * worst_torch), (worst, worst_torch)
     # x < d triangle is exactly zero everywhere
     tri = torch.arange(960, device="cuda")[None, :] < torch.arange(192, device="cuda")[:, None]
@@ -702,6 +705,32 @@ def test_fused_soft_argmin_nonfinite_and_empty():
     assert vol0.shape == (1, 0, 2, 8) and torch.equal(disp0, torch.zeros(1, 1, 2, 8, device="cuda"))
 
 
+@pytest.mark.parametrize("mean", [False, True])
+@pytest.mark.parametrize("kind", ["nonfinite", "tiny"])
+def test_fused_volume_free_multipass_exact_segments(kind, mean):
+    """D = 256 without the volume (two passes + merge) on segments that take the band kernel's
+    exact fp32 path: +-inf / NaN features, or a feature scale the fp16 split cannot reach
+    (max |L| ~ 2^-91).  Each pass must leave its partial softmax state in the workspace (NaN
+    carried as NaN), so the merged disparity equals the two-kernel pipeline's."""
+    from realtime_stereo_matcher_amd import functional as F
+
+    l, r = _feats(24 if kind == "nonfinite" else 25, (1, 16, 3, 320))
+    if kind == "nonfinite":
+        l[0, 5, 0, 300] = np.inf     # pass 0 and pass 1 cells of row 0
+        l[0, 0, 1, 7] = -np.inf
+        r[0, 3, 1, 100] = np.nan     # NaN in one pass only for some pixels
+        r[0, 9, 2, 3] = np.inf
+    else:
+        l, r = (l * 1e-28).astype(np.float32), (r * 1e-8).astype(np.float32)
+    L, R = dev(l), dev(r)
+    _, disp = F.inner_product_soft_argmin(L, R, 256, mean=mean, keep_volume=False)
+    vol = F.correlation_volume(L, R, 256) if mean else F.inner_product_volume(L, R, 256)
+    want = O.softargmin(host(vol))
+    got = host(disp)
+    np.testing.assert_array_equal(np.isnan(got), np.isnan(want))
+    np.testing.assert_allclose(got, want, atol=TOL, rtol=0, equal_nan=True)
+
+
 def test_cfg2_fused_full_size():
     """cfg2 through the fused kernel: the volume equals the volume op's bit for bit, the
     disparity is the fp64 soft-argmin of that volume, with or without the volume written."""
@@ -758,7 +787,15 @@ def test_warp_strided_and_errors():
     with pytest.raises(AssertionError, match="invalid flow map dimension"):
         warp_by_flow_map(I, torch.zeros(2, 3, 10, 24, device="cuda"))
     with pytest.raises(TypeError):
-        warp_by_flow_map(I.half(), Fl[:, :1].half())
+        warp_by_flow_map(I.double(), Fl[:, :1].double())
+    with pytest.raises(RuntimeError):  # mixed dtypes outside autocast, as grid_sample
+        warp_by_flow_map(I.half(), Fl[:, :1])
+    # fp16 image and flow outside autocast: sampled in fp32 from the fp16 values, rounded once
+    ih, fh = I.half(), Fl[:, :1].half()
+    got = warp_by_flow_map(ih, fh)
+    assert got.dtype == torch.float16
+    want = O.warp_by_flow_map(host(ih), host(fh))
+    np.testing.assert_allclose(host(got), want, atol=2e-3, rtol=2.0 ** -10)
     with pytest.raises(RuntimeError):
         warp_by_flow_map(I.cpu(), Fl[:, :1].cpu())
 

@@ -106,3 +106,26 @@ def test_v4_volume_strided_and_errors():
         F.v4_volume(big[:, :16], big[:, :16], *ws, 48)
     with pytest.raises(TypeError):
         F.v4_volume(L.half(), R.half(), *ws, 48)
+
+
+def test_v4_volume_network_shape_sampled_rows():
+    """The V4 network's own volume shape (1x32x96x312, D = 48: KITTI-like 384x1248 input at 1/4
+    resolution, model/mobile_stereo_net_v4.py:443-461): sampled rows against the fp64 oracle.
+    Row y depends on feature rows y-3 .. y+3 (three 3x3 layers), so the oracle runs on that band;
+    the band's own edges are the image's edges only at y = 0 and y = H-1, where that is exact."""
+    from realtime_stereo_matcher_amd import functional as F
+    from realtime_stereo_matcher_amd.model.mobile_stereo_net_v4 import fold_v4_weights
+
+    n, c, h, w, D = 1, 32, 96, 312, 48
+    c3d, v11 = _stacks(seed=17)
+    g = torch.Generator(device="cuda").manual_seed(9)
+    L = torch.randn(n, c, h, w, device="cuda", generator=g)
+    R = torch.randn(n, c, h, w, device="cuda", generator=g)
+    with torch.no_grad():
+        got = F.v4_volume(L, R, *fold_v4_weights(c3d, v11), D).cpu().numpy()
+    fl, fr = L.cpu().numpy(), R.cpu().numpy()
+    p = _params(c3d, v11)
+    for y in (0, 1, 47, 94, 95):
+        y0, y1 = max(0, y - 3), min(h, y + 4)
+        want = O.v4_volume(fl[:, :, y0:y1], fr[:, :, y0:y1], p, D)[:, :, y - y0]
+        np.testing.assert_allclose(got[:, :, y], want, atol=TOL, rtol=0)

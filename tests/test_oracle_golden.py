@@ -210,3 +210,52 @@ def test_v4_volume(name):
     against the reference loop's own output."""
     a, p = v4_case(name)
     np.testing.assert_allclose(O.v4_volume(a["featL"], a["featR"], p, 48), a["volume"], atol=1e-5, rtol=0)
+
+
+# ------------------------------------------------- eager restatements of the isolation test
+@pytest.mark.parametrize("rec", cases("diff_volume"), ids=_ids(cases("diff_volume")))
+def test_torch_port_diff_volume(rec):
+    a = load_case(rec)
+    dt = {"f32": torch.float32, "f16": torch.float16, "bf16": torch.bfloat16}[rec["dtype"]]
+    got = P.sweep_diff_volume(torch.from_numpy(a["left"]).to(dt), torch.from_numpy(a["right"]).to(dt),
+                              rec["params"]["max_disp"])
+    np.testing.assert_array_equal(got.float().numpy(), a["out"].astype(np.float32))
+
+
+@pytest.mark.parametrize("rec", cases("softargmin"), ids=_ids(cases("softargmin")))
+def test_torch_port_softargmin_fp64(rec):
+    a = load_case(rec)
+    got = P.soft_argmin_fp64(torch.from_numpy(a["volume"])).numpy()
+    np.testing.assert_allclose(got, O.softargmin(a["volume"]), atol=1e-6, rtol=0)
+    np.testing.assert_allclose(got, a["out"], atol=TOL_F32, rtol=0)
+
+
+@pytest.mark.parametrize("rec", cases("regression_presoftmax"), ids=_ids(cases("regression_presoftmax")))
+def test_torch_port_presoftmax_fp64(rec):
+    a = load_case(rec)
+    got = P.regression_presoftmax_fp64(torch.from_numpy(a["volume"]), rec["params"]["maxdisp"]).numpy()
+    np.testing.assert_allclose(got, a["out"], atol=TOL_F32, rtol=0)
+
+
+@pytest.mark.parametrize("rec", cases("warp"), ids=_ids(cases("warp")))
+def test_torch_port_warp(rec):
+    a = load_case(rec)
+    got = P.warp_grid_sample(torch.from_numpy(a["image"]), torch.from_numpy(a["flow"])).numpy()
+    np.testing.assert_allclose(got, a["out"], atol=TOL_F32, rtol=0, equal_nan=True)
+
+
+@pytest.mark.parametrize("name", V4_FILES)
+def test_torch_port_v4_volume_loop(name):
+    """The eager V4 loop on modules loaded with the fixture's parameters reproduces the reference
+    loop's output (the isolation test swaps it in for the HIP operator)."""
+    from realtime_stereo_matcher_amd.model.stereo_net_v4 import MobileStereoNetV4HIP
+
+    a, p = v4_case(name)
+    net = MobileStereoNetV4HIP(192)
+    net.conv3d.load_state_dict({k[7:]: torch.from_numpy(v) for k, v in p.items() if k.startswith("conv3d.")})
+    net.volume11.load_state_dict({k[9:]: torch.from_numpy(v) for k, v in p.items() if k.startswith("volume11.")})
+    net.eval()
+    with torch.no_grad():
+        got = P.v4_volume_loop(torch.from_numpy(a["featL"]), torch.from_numpy(a["featR"]),
+                               net.conv3d, net.volume11, 48).numpy()
+    np.testing.assert_allclose(got, a["volume"], atol=1e-5, rtol=0)
