@@ -58,7 +58,8 @@
 
 #ifndef SMCV_ABLATE
 #define SMCV_ABLATE 0  // diagnostics only (scripts/ip_stamps.hip): 1 no MFMA, 2 all feature
-#endif                 // loads from one line, 4 no stores, 8 no epilogue
+#endif                 // loads from one line, 4 no stores, 8 no epilogue, 16 no staging
+                       // (planes not written), 32 no shear (accumulators stored unsheared)
 #ifndef SMCV_PREFETCH
 #define SMCV_PREFETCH 0  // L2 touches two steps ahead (1: on; measured slower on cfg2, r01)
 #endif
@@ -208,31 +209,34 @@ __device__ __forceinline__ void vm_wait(QT (&v)[8], unsigned& pf, int after_stor
 
 // 4 fp32 results -> storage type (round to nearest even; NaN stays NaN, overflow gives inf).
 // Global address space explicitly: a flat store would count in vmcnt out of order.
-template <typename T>
-__device__ __forceinline__ void store_quad(T* p, f32x4v v, bool nt = true) {
+// NT (compile time, so each instantiation holds ONE kind of store: an if / else of a
+// non-temporal and a plain store to one address is merged by the compiler into a plain store,
+// dropping the non-temporal hint -- that silently happened to every fp32 volume store in r02):
+//   true: non-temporal -- the volume is written once and never re-read by this kernel; plain
+//         stores allocate its lines in L2 and evict the feature lines the loads reuse
+//         (scripts/micro/mlp_patterns.hip: cfg2 reads + writes 140 us plain vs 106 us nt);
+//   false: plain -- fp32 rows with W % 4 != 0, whose 128-B row pieces straddle two lines: L2
+//         merges the two halves of a line before it writes the line back.
+template <bool NT, typename T>
+__device__ __forceinline__ void store_quad(T* p, f32x4v v) {
   typedef __attribute__((address_space(1))) void gvoid;
   gvoid* g = (gvoid*)p;
-  // non-temporal: the volume is written once and never re-read by this kernel; plain stores
-  // would allocate its lines in L2 and evict the feature lines the loads reuse
-  // (scripts/micro/mlp_patterns.hip: cfg2 reads + writes 140 us plain vs 106 us nt).
-  // nt == false (fp32 rows with W % 4 != 0, whose 128-B row pieces straddle two lines): plain
-  // stores, so that L2 merges the two halves of a line before it writes the line back.
   if constexpr (sizeof(T) == 4) {
-    if (SMCV_NT_STORE && nt)
+    if constexpr (SMCV_NT_STORE && NT)
       __builtin_nontemporal_store(v, reinterpret_cast<__attribute__((address_space(1))) f32x4v*>(g));
     else
       *reinterpret_cast<__attribute__((address_space(1))) f32x4v*>(g) = v;
   } else if constexpr (std::is_same<T, __half>::value) {
     typedef _Float16 h4 __attribute__((ext_vector_type(4)));
     const h4 r = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
-    if (SMCV_NT_STORE)
+    if constexpr (SMCV_NT_STORE && NT)
       __builtin_nontemporal_store(r, reinterpret_cast<__attribute__((address_space(1))) h4*>(g));
     else
       *reinterpret_cast<__attribute__((address_space(1))) h4*>(g) = r;
   } else {
     typedef __bf16 b4 __attribute__((ext_vector_type(4)));
     const b4 r = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
-    if (SMCV_NT_STORE)
+    if constexpr (SMCV_NT_STORE && NT)
       __builtin_nontemporal_store(r, reinterpret_cast<__attribute__((address_space(1))) b4*>(g));
     else
       *reinterpret_cast<__attribute__((address_space(1))) b4*>(g) = r;
@@ -257,6 +261,20 @@ __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
   return v;
+}
+
+// The fp32 split of two values x (channels 2q, 2q+1 of one pixel), scaled by sc = 2^k (exact):
+// h = rn16(x sc) and m = rn16(x sc - h), packed as (lo, hi) fp16 pairs.  Four v_fma_mix*, i.e.
+// two VALU per value (the compiler's cvt / cvt-back / subtract / pack sequence took four): the
+// mix forms evaluate x * sc - h exactly (x sc is exact, and h is its rounding, so the difference
+// is an fp32 number) and round it to fp16 once -- bit-identical to that sequence.
+__device__ __forceinline__ void split_pair(float a, float b, float sc, unsigned& h, unsigned& m) {
+  asm("v_fma_mixlo_f16 %0, %2, %4, 0\n\t"
+      "v_fma_mixhi_f16 %0, %3, %4, 0\n\t"
+      "v_fma_mixlo_f16 %1, %2, %4, -%0 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %1, %3, %4, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(h), "=&v"(m)
+      : "v"(a), "v"(b), "v"(sc));
 }
 
 // exponent e with x = f 2^e, f in [0.5, 1) (x > 0 finite)
@@ -377,69 +395,59 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
   float mx = 0.f;      // this lane's max|x| over the current segment (fp32 only)
   // stage one step into the plane(s)
   auto put = [&](Set& st) {
-    if (!active) return;
+    if (!active || (SMCV_ABLATE & 16)) return;
     if constexpr (NP == 2) {
-      float4 v[8];
+      const float sc = __builtin_ldexpf(1.0f, isR ? kR : kL);  // 2^k (1.0 when unscaled)
+      // max |x| and the split, straight from the loaded registers (no copies): v_max3 with |.|
+      // modifiers, two values per instruction in two chains (fmaxf would canonicalise every
+      // loaded value first), then four v_fma_mix per value pair
+      auto stage = [&](const f32x4v (&v)[8]) {
+        float m0 = mx, m1 = 0.f;
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk)
-        v[kk] = make_float4(st.v[kk].x, st.v[kk].y, st.v[kk].z, st.v[kk].w);
-      if (__any(st.nv != 8)) {  // row edges / channel tail only
-        const int nv = st.nv & 15;
-#pragma unroll
-        for (int kk = 0; kk < 8; ++kk)
-          if (kk >= nv) v[kk] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (st.nv & 16) {  // loaded from W - 4: pixels W - r .. W - 1 move to lanes' slots 0 .. r-1
-          const int r = W & 3;
-#pragma unroll
-          for (int kk = 0; kk < 8; ++kk) {
-            const float4 o = v[kk];
-            v[kk] = r == 1 ? make_float4(o.w, 0.f, 0.f, 0.f)
-                  : r == 2 ? make_float4(o.z, o.w, 0.f, 0.f)
-                           : make_float4(o.y, o.z, o.w, 0.f);
-          }
+        for (int kk = 0; kk < 8; ++kk) {
+          asm("v_max3_f32 %0, %0, |%1|, |%2|" : "+v"(m0) : "v"(v[kk].x), "v"(v[kk].y));
+          asm("v_max3_f32 %0, %0, |%1|, |%2|" : "+v"(m1) : "v"(v[kk].z), "v"(v[kk].w));
         }
-      }
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk)
-        mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v[kk].x), fabsf(v[kk].y)),
-                             fmaxf(fabsf(v[kk].z), fabsf(v[kk].w))));
-      float col[4][8];
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
-        col[0][kk] = v[kk].x;
-        col[1][kk] = v[kk].y;
-        col[2][kk] = v[kk].z;
-        col[3][kk] = v[kk].w;
-      }
-      auto split = [&](float sc, auto scaled) {
+        mx = fmaxf(m0, m1);
+        // swz(4g + p, ch) = swz(4g, ch) ^ 32 p (p only flips the row bits 5-6, which hold g & 3):
+        // one opaque base per step, so the compiler keeps one register instead of four
+        // loop-invariant offsets (which spilled, and every reload waited for vmcnt(0))
+        unsigned o0 = (unsigned)swz(4 * g, ch);
+        asm volatile("" : "+v"(o0));
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
           uint4 wh, wm;
-          unsigned* ph = reinterpret_cast<unsigned*>(&wh);
-          unsigned* pm = reinterpret_cast<unsigned*>(&wm);
-#pragma unroll
-          for (int qq = 0; qq < 4; ++qq) {
-            const float a = col[p][2 * qq], b = col[p][2 * qq + 1];
-            const float as = decltype(scaled)::value ? a * sc : a;
-            const float bs = decltype(scaled)::value ? b * sc : b;
-            const hp2 hv = {(_Float16)as, (_Float16)bs};  // v_cvt_pk_f16_f32: nearest even
-            const float ra = decltype(scaled)::value ? __builtin_fmaf(a, sc, -(float)hv[0])
-                                                     : a - (float)hv[0];
-            const float rb = decltype(scaled)::value ? __builtin_fmaf(b, sc, -(float)hv[1])
-                                                     : b - (float)hv[1];
-            const hp2 mv = {(_Float16)ra, (_Float16)rb};
-            ph[qq] = __builtin_bit_cast(unsigned, hv);
-            pm[qq] = __builtin_bit_cast(unsigned, mv);
-          }
-          const int off = swz(4 * g + p, ch);
+          split_pair(v[0][p], v[1][p], sc, wh.x, wm.x);
+          split_pair(v[2][p], v[3][p], sc, wh.y, wm.y);
+          split_pair(v[4][p], v[5][p], sc, wh.z, wm.z);
+          split_pair(v[6][p], v[7][p], sc, wh.w, wm.w);
+          const unsigned off = o0 ^ (32u * p);
           *reinterpret_cast<uint4*>(smem + off) = wh;
           *reinterpret_cast<uint4*>(smem + G::PLANE + off) = wm;
         }
       };
-      if (__builtin_amdgcn_readfirstlane(kL | kR) == 0) {  // uniform: a scalar branch
-        split(1.0f, std::false_type{});
+      if (__builtin_expect(__any(st.nv != 8), 0)) {  // row edges / channel tail only
+        f32x4v v[8];
+        const int nv = st.nv & 15;
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) v[kk] = kk < nv ? st.v[kk] : f32x4v{0.f, 0.f, 0.f, 0.f};
+        if (st.nv & 16) {  // loaded from W - 4: pixels W - r .. W - 1 move to lanes' slots 0 .. r-1
+          const int r = W & 3;  // 1, 2 or 3 (uniform); element-wise selects
+          const bool r1 = r == 1, r2 = r == 2;
+#pragma unroll
+          for (int kk = 0; kk < 8; ++kk) {
+            const f32x4v o = v[kk];
+            f32x4v n;
+            n.x = r1 ? o.w : (r2 ? o.z : o.y);
+            n.y = r1 ? 0.f : (r2 ? o.w : o.z);
+            n.z = (r1 || r2) ? 0.f : o.w;
+            n.w = 0.f;
+            v[kk] = n;
+          }
+        }
+        stage(v);
       } else {
-        split(__builtin_ldexpf(1.0f, isR ? kR : kL), std::true_type{});
+        stage(st.v);
       }
     } else {
       // 16-bit features as they are: 8 channels x 4 pixels -> 4 rows of 8 channels
@@ -629,7 +637,8 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
 
   // SCALE: multiply back by 2^-(kL+kR); XLT: the segment has cells x < d (R pad rows), forced
   // to 0.  Compile-time, so the common case costs no VALU.
-  auto epilogue_v = [&](const Work& k, bool fast, auto scale, auto xlt) {
+  auto epilogue_v = [&](const Work& k, bool fast, auto scale, auto xlt, auto ntc) {
+    constexpr bool NTQ = decltype(ntc)::value;
     const int x0w = k.x0 + 32 * wave;  // this wave's first pixel
     const float mul = args.mul;
     const int kk = -(kL + kR);
@@ -660,17 +669,24 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
           if (sA != 2) {
             addr = wb + (unsigned)(sB * kSlot - ci * 128);
           } else {  // chunk a in slot 2, chunk a+1 in slot 0
-            addr = wb + (unsigned)(3 * kSlot - ci * 128) - (uu >= ci ? 3u * kSlot : 0u);
+            // the wrap amount is selected, kept opaque, and subtracted; the constant part folds
+            // into the ds_write offset (left to itself the compiler hoists 32 constants, one pair
+            // per element, into VGPRs for the whole kernel -- which then spilled)
+            unsigned sel = uu >= ci ? 3u * kSlot : 0u;
+            asm volatile("" : "+v"(sel));
+            addr = (wb - sel) + (unsigned)(3 * kSlot - ci * 128);
           }
         } else {
           const int bp = 32 * ((a + 4) % 3);  // ring d-position of local disparity 32 (a+1)
           if (bp != 0) {
             addr = wb + (unsigned)(4 * (bp - ci));
-          } else {  // u < c_i wraps to the top of the 96-entry circle
-            addr = wb + (unsigned)(4 * (96 - ci)) - (uu >= ci ? 384u : 0u);
+          } else {  // u < c_i wraps to the top of the 96-entry circle (wrap kept opaque, as above)
+            unsigned sel = uu >= ci ? 384u : 0u;
+            asm volatile("" : "+v"(sel));
+            addr = (wb - sel) + (unsigned)(4 * (96 - ci));
           }
         }
-        lds_store1(addr, val);
+        if (!(SMCV_ABLATE & 32)) lds_store1(addr, val);
       }
       // the wave's own ring writes precede its reads (LDS executes a wave's operations in order)
       asm volatile("" ::: "memory");
@@ -680,7 +696,10 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
         for (int qq = 0; qq < 4; ++qq) {
           const unsigned ra = LAYOUT == kNDHW ? rb + (unsigned)((a % 3) * kSlot + 8 * qq * 128)
                                               : rb + (unsigned)(8 * qq * 384 + (a % 3) * 128);
-          v[qq] = lds_load4(ra);
+          if constexpr ((SMCV_ABLATE & 32) != 0)
+            v[qq] = f32x4v{acc[t][4 * qq], acc[t][4 * qq + 1], acc[t][4 * qq + 2], acc[t][4 * qq + 3]};
+          else
+            v[qq] = lds_load4(ra);
         }
 
         if (store_vol) {
@@ -694,7 +713,7 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
 #pragma unroll
               for (int qq = 0; qq < 4; ++qq) {
                 asm volatile("" : "+v"(ol));
-                store_quad<TO>(ol, v[qq], ntq);
+                store_quad<NTQ>(ol, v[qq]);
                 ol += st8;
               }
             } else {
@@ -705,7 +724,7 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
                 const int xq = x0w + 4 * clo;
                 if (dl < k.Dp && xq < W && !(SMCV_ABLATE & 4)) {
                   if (xq + 4 <= W) {
-                    store_quad<TO>(ol, v[qq], ntq);
+                    store_quad<NTQ>(ol, v[qq]);
                   } else {  // the row's last, partial quad (W % 4 != 0)
 #pragma unroll
                     for (int e = 0; e < 3; ++e)
@@ -721,14 +740,14 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
             asm volatile("" : "+v"(ol));
             if (fast) {
 #pragma unroll
-              for (int qq = 0; qq < 4; ++qq) store_quad<TO>(ol + (size_t)(8 * qq) * D, v[qq]);
+              for (int qq = 0; qq < 4; ++qq) store_quad<true>(ol + (size_t)(8 * qq) * D, v[qq]);
             } else {
               const int d0 = 32 * a + 4 * clo;
 #pragma unroll
               for (int qq = 0; qq < 4; ++qq) {
                 if (x0w + 8 * qq + rlo >= W || (SMCV_ABLATE & 4)) continue;
                 if (d0 + 4 <= k.Dp && dq) {
-                  store_quad<TO>(ol + (size_t)(8 * qq) * D, v[qq]);
+                  store_quad<true>(ol + (size_t)(8 * qq) * D, v[qq]);
                 } else {
 #pragma unroll
                   for (int e = 0; e < 4; ++e)
@@ -744,23 +763,30 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
     }
   };
 
-  auto epilogue = [&](const Work& k, bool fast) {
+  auto epilogue_n = [&](const Work& k, bool fast, auto ntc) {
     using TT = std::true_type;
     using FF = std::false_type;
     const bool xl = __builtin_amdgcn_readfirstlane(k.js) < 0;
     if constexpr (NP == 2) {
       if (__builtin_amdgcn_readfirstlane(kL + kR) != 0) {
         if (xl)
-          epilogue_v(k, fast, TT{}, TT{});
+          epilogue_v(k, fast, TT{}, TT{}, ntc);
         else
-          epilogue_v(k, fast, TT{}, FF{});
+          epilogue_v(k, fast, TT{}, FF{}, ntc);
         return;
       }
     }
     if (xl)
-      epilogue_v(k, fast, FF{}, TT{});
+      epilogue_v(k, fast, FF{}, TT{}, ntc);
     else
-      epilogue_v(k, fast, FF{}, FF{});
+      epilogue_v(k, fast, FF{}, FF{}, ntc);
+  };
+  // non-temporal NDHW stores unless an fp32 row's 16-B pieces straddle lines (W % 4 != 0)
+  auto epilogue = [&](const Work& k, bool fast) {
+    if (LAYOUT != kNDHW || ntq)
+      epilogue_n(k, fast, std::true_type{});
+    else
+      epilogue_n(k, fast, std::false_type{});
   };
 
   // exact fp32 path for a segment holding +-inf (or a scale fp32 cannot reach)

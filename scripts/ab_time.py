@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Median / min launch time of the hot-path kernels at the bench workloads, for same-box A/B of
+library builds (STEREOCV_LIB=path selects the .so).  One JSON line per op.
+    STEREOCV_LIB=... python scripts/ab_time.py [--ops cfg2,cfg3,...] [--reps 25] [--tag name]"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from realtime_stereo_matcher_amd import functional as F  # noqa: E402
+
+
+def feats(shape, dtype):
+    g = torch.Generator(device="cuda").manual_seed(1234)
+    return (torch.randn(*shape, device="cuda", generator=g).to(dtype),
+            torch.randn(*shape, device="cuda", generator=g).to(dtype))
+
+
+def ops():
+    return {
+        # name: (setup -> callable, pairs per launch, algorithmic bytes per pair)
+        "cfg2": (lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192))(*feats((8, 64, 540, 960), torch.float32)),
+                 8, 663552000),
+        "cfg2_fused_nv": (lambda: (lambda L, R: lambda: F.inner_product_soft_argmin(L, R, 192, keep_volume=False))(
+            *feats((8, 64, 540, 960), torch.float32)), 8, 267494400),
+        "cfg2_regress": (lambda: (lambda v: lambda: F.soft_argmin(v))(torch.randn(8, 192, 540, 960, device="cuda")),
+                         8, 400204800),
+        "cfg3": (lambda: (lambda L, R: lambda: F.groupwise_volume(L, R, 8, 192))(*feats((1, 256, 540, 960), torch.bfloat16)),
+                 1, 3715891200),
+        "cfg4": (lambda: (lambda L, R: lambda: F.correlation_volume(L, R, 256))(*feats((4, 16, 1080, 1920), torch.float32)),
+                 4, 2388787200),
+        "cfg4_fused_nv": (lambda: (lambda L, R: lambda: F.inner_product_soft_argmin(L, R, 256, mean=True, keep_volume=False))(
+            *feats((4, 16, 1080, 1920), torch.float32)), 4, 273715200),
+        "cfg5": (lambda: (lambda L, R: lambda: F.concat_volume(L, R, 64))(*feats((1, 128, 540, 960), torch.float16)),
+                 1, 17252352000),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ops", default="cfg2")
+    ap.add_argument("--reps", type=int, default=25)
+    ap.add_argument("--tag", default=os.environ.get("STEREOCV_LIB", "default"))
+    a = ap.parse_args()
+    table = ops()
+    for name in a.ops.split(","):
+        setup, pairs, nbytes = table[name]
+        fn = setup()
+        for _ in range(5):
+            fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(a.reps):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            fn()
+            e.record()
+            e.synchronize()
+            ts.append(s.elapsed_time(e) * 1e3)
+        ts.sort()
+        med = ts[len(ts) // 2]
+        print(json.dumps({"tag": os.path.basename(a.tag), "op": name, "median_us": round(med, 1),
+                          "min_us": round(ts[0], 1), "us_per_pair": round(med / pairs, 2),
+                          "frac": round(nbytes * pairs / (med * 1e-6) / 8e12, 4)}), flush=True)
+        del fn
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

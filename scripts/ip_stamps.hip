@@ -8,9 +8,11 @@
 #include "../realtime_stereo_matcher_amd/csrc/ip_f32.hip"
 #include "../realtime_stereo_matcher_amd/csrc/ip_h2.hip"
 
+#ifdef SMCV_STAMPS
 namespace smcv {
 __device__ unsigned long long g_stamps[4096][kStampPhases];
 }
+#endif
 
 #include <cstdio>
 #include <cstdint>
@@ -22,7 +24,8 @@ int main(int argc, char** argv) {
   // fusednv (soft-argmin only), gw (groupwise bf16 cfg3: C=256, G=8, fp32 (N,G,H,W,D) out)
   const char* mode = argc > 2 ? argv[2] : "bf16x3";
   const bool gw = !strcmp(mode, "gw");
-  const int64_t N = 1, C = gw ? 256 : 64, H = 540, W = 960, D = argc > 1 ? atoi(argv[1]) : 192;
+  const int64_t N = argc > 3 ? atoi(argv[3]) : 1, C = gw ? 256 : 64, H = 540, W = 960,
+                D = argc > 1 ? atoi(argv[1]) : 192;
   const int64_t G = 8;
   const size_t nin = N * C * H * W, nout = gw ? N * G * H * W * D : N * D * H * W;
   const size_t esz = gw ? 2 : 4;
@@ -68,7 +71,9 @@ int main(int argc, char** argv) {
   hipDeviceSynchronize();
   static unsigned long long zero[4096][12];
   memset(zero, 0, sizeof(zero));
+#ifdef SMCV_STAMPS
   hipMemcpyToSymbol(HIP_SYMBOL(smcv::g_stamps), zero, sizeof(zero));
+#endif
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
@@ -79,7 +84,11 @@ int main(int argc, char** argv) {
   float ms = 0;
   hipEventElapsedTime(&ms, a, b);
   static unsigned long long st[4096][12];
+#ifdef SMCV_STAMPS
   hipMemcpyFromSymbol(st, HIP_SYMBOL(smcv::g_stamps), sizeof(st));
+#else
+  memset(st, 0, sizeof(st));
+#endif
   const char* names[12] = {"top barrier", "stage (split+lds)", "stage barrier", "mfma",
                            "epi barrier 1", "shear writes", "epi barrier 2", "store loop",
                            "stage: dma wait", "dma issue", "-", "-"};

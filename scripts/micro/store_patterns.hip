@@ -82,6 +82,9 @@ int main() {
   SEG(8, 2, false, 256) SEG(16, 2, true, 256) SEG(4, 2, true, 512) SEG(4, 2, true, 1024)
   SEG(8, 2, true, 512) SEG(4, 4, true, 256) SEG(8, 8, true, 512)
   SEG(4, 2, true, 4320) SEG(8, 2, true, 4320)
+  // the band kernel's chunk stores: 8 rows x 128 B (32-pixel waves) vs 16 rows x 64 B (16-pixel)
+  SEG(4, 8, true, 512) SEG(4, 8, false, 512) SEG(4, 16, true, 512) SEG(4, 16, false, 512)
+  SEG(8, 8, true, 512)  // (ROWS must divide D / NW = 24 rows per wave: no 16-row variant at NW=8)
   rep("rows nt", timeit([&] { row_store<true><<<dim3(H, D / 16), 256>>>(out); }));
   rep("rows", timeit([&] { row_store<false><<<dim3(H, D / 16), 256>>>(out); }));
   hipFree(out);
