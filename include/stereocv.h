@@ -51,9 +51,11 @@ enum sm_ip_algo {
   SM_IP_MFMA_F32 = 2,    /* banded C-contraction on v_mfma_f32_16x16x4_f32 (exact fp32 fma) */
   SM_IP_MFMA_BF16X3 = 3, /* banded C-contraction on bf16 MFMA over an exact 3-way bf16 split */
   /* 4: reserved (a retired warp-specialised variant of the bf16 split) */
-  SM_IP_MFMA_H2 = 5      /* banded contraction on 32x32x16 MFMA, two workgroups per CU, every wave
+  SM_IP_MFMA_H2 = 5,     /* banded contraction on 32x32x16 MFMA, two workgroups per CU, every wave
                             loads, stages, multiplies and stores (the default) */
   /* 6: reserved (a retired warp-specialised variant, removed in round 3) */
+  SM_IP_MFMA_B16 = 7     /* the same contraction re-tiled on 16x16x32 MFMA: 16-pixel waves, four
+                            waves per SIMD (fp32, 4-element aligned rows; other shapes: MFMA_H2) */
 };
 
 /* Library version (major*10000 + minor*100 + patch). */

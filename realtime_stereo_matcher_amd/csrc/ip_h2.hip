@@ -46,50 +46,19 @@
 // relative to the chunk's first row, across chunks in fp64); the 8 lanes of a pixel column
 // merge by cross-lane shuffles after the last chunk, so the segment's disparities leave the
 // same pass -- with or without the volume.
-#include "common.h"
-
-#include <math.h>
-
-#include <type_traits>
-
-#ifndef SMCV_NT_STORE
-#define SMCV_NT_STORE 1  // volume stores non-temporal (0: plain, for A/B)
-#endif
-
-#ifndef SMCV_ABLATE
-#define SMCV_ABLATE 0  // diagnostics only (scripts/ip_stamps.hip): 1 no MFMA, 2 all feature
-#endif                 // loads from one line, 4 no stores, 8 no epilogue, 16 no staging
-                       // (planes not written), 32 no shear (accumulators stored unsheared)
-#ifndef SMCV_PREFETCH
-#define SMCV_PREFETCH 0  // L2 touches two steps ahead (1: on; measured slower on cfg2, r01)
-#endif
+#include "band_common.h"
 
 namespace smcv {
 namespace h2band {
 
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef _Float16 hp2 __attribute__((ext_vector_type(2)));
-typedef float f32x4v __attribute__((ext_vector_type(4)));
-typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-
 constexpr int kWaves = 4;
 constexpr int kThreads = 64 * kWaves;
-constexpr int kXT = 32 * kWaves;    // left pixels per row segment
 constexpr int kKC = 16;             // channels per step (one 32x32x16 k-step)
 constexpr int kRowB = 32;           // bytes per plane row: 16 x 16-bit
 constexpr int kSlot = 32 * 32 * 4;  // one ring chunk: 32 x 32 fp32
 constexpr int kRingW = 3 * kSlot;   // a wave's ring
-constexpr int kPF = SMCV_PREFETCH ? 1 : 0;  // touch instructions issued after each step's loads
 enum { kNDHW = 0, kNGHWD = 1 };
 
-// byte offset of (plane row r, 8-channel chunk h).  Fragment reads: lane l -> row base + (l & 31),
-// chunk l >> 5; plane writes: 8 consecutive lanes -> rows 4i + p of one 32-row block.  Both are
-// conflict-free under the gfx950 ds_read_b128 / ds_write_b128 lane groups (scripts/check_swizzle.py).
-__device__ __forceinline__ int swz(int r, int h) {
-  return ((r ^ ((r >> 2) & 3)) << 5) + ((h ^ ((r >> 4) & 1)) << 4);
-}
 
 template <typename T, int TMAX>
 struct Geo {
@@ -108,177 +77,10 @@ struct Geo {
   static_assert(SHM * 2 <= 160 * 1024, "two workgroups per CU");
 };
 
-struct Args {
-  const void* L;
-  const void* R;
-  void* out;    // volume; nullptr: not stored (fused kernel only)
-  float* disp;  // fused kernel: (N, H, W) disparities
-  int C, cpg, G, H, W, D;
-  Strides4 ls, rs;
-  int tiles, npass, pw, nwork;
-  float mul;  // MEAN: 1 / (channels averaged)
-  // volume-free fused kernel with npass > 1: each pass's partial soft-argmin state per pixel
-  // (max, sum e, sum d e relative to that max), merged by fused_merge_kernel
-  double* ws_s;
-  double* ws_t;
-  float* ws_m;
-  int64_t nhw;  // N H W: the workspace's per-pass stride
-};
 
-struct Work {
-  int n, y, g, x0, dp, Dp, js, pass;
-};
 
-// work index w = (((n H + y) G + g) tiles + tile) npass + pass: consecutive items are
-// neighbouring segments of one row (and group), which share right-window columns in L2
-__device__ __forceinline__ Work decode(int w, const Args& a, int dmax) {
-  Work k;
-  const int pass = w % a.npass;
-  const int r1 = w / a.npass;
-  const int tile = r1 % a.tiles;
-  const int r2 = r1 / a.tiles;
-  k.g = r2 % a.G;
-  const int row = r2 / a.G;
-  k.y = row % a.H;
-  k.n = row / a.H;
-  k.x0 = tile * kXT;
-  k.dp = pass * a.pw;
-  k.pass = pass;
-  k.Dp = min(a.pw, a.D - k.dp);
-  k.js = k.x0 - k.dp - dmax;
-  return k;
-}
 
-typedef __attribute__((address_space(3))) unsigned char lds_u8;
-__device__ __forceinline__ unsigned lds_addr(const void* p) {
-  return (unsigned)(uintptr_t)(const lds_u8*)p;
-}
-__device__ __forceinline__ void lds_store1(unsigned addr, float v) {
-  *reinterpret_cast<__attribute__((address_space(3))) float*>(addr) = v;
-}
-__device__ __forceinline__ float lds_load1(unsigned addr) {
-  return *reinterpret_cast<__attribute__((address_space(3))) float*>(addr);
-}
-__device__ __forceinline__ f32x4v lds_load4(unsigned addr) {
-  return *reinterpret_cast<__attribute__((address_space(3))) f32x4v*>(addr);
-}
-__device__ __forceinline__ __attribute__((address_space(3))) unsigned* lds_word(unsigned addr) {
-  return reinterpret_cast<__attribute__((address_space(3))) unsigned*>(addr);
-}
 
-// a 4-pixel group of one channel row in registers: 16 B (fp32) or 8 B (fp16 / bf16)
-template <typename T> struct Quad { using type = u32x2; };
-template <> struct Quad<float> { using type = f32x4v; };
-
-// Feature loads are issued by inline asm so that the compiler neither waits for them itself
-// (its control-flow merges would put vmcnt(0) -- a wait for every output store in flight --
-// in front of every step) nor knows them: the kernel counts vmcnt by hand (vm_wait).
-template <bool ASM, typename QT>
-__device__ __forceinline__ void gload(QT& v, const void* p) {
-  if constexpr (!ASM) {  // compiler-tracked (the fused kernels: see band_h2)
-    typedef __attribute__((address_space(1))) const void gcvoid;
-    v = *reinterpret_cast<__attribute__((address_space(1))) const QT*>((gcvoid*)p);
-  } else if constexpr (sizeof(QT) == 16) {
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-  } else {
-    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-  }
-}
-
-// Wait for the feature loads: vmcnt(N + NPF) when N output stores were issued after them (they
-// may stay in flight, as may the NPF touches issued right after the loads), else vmcnt(NPF).
-// One asm statement with the scalar branch inside, and the loaded registers (and the touch
-// destination) as tied operands: no use of them is scheduled before the wait, and the register
-// allocator has a single place (the load's destination) to keep them.
-template <int N, int NPF, bool ASM = true, typename QT>
-__device__ __forceinline__ void vm_wait(QT (&v)[8], unsigned& pf, int after_stores) {
-  if constexpr (!ASM) return;  // compiler-tracked loads: the compiler places the waits
-  asm volatile(
-      "s_cmp_eq_u32 %9, 0\n\t"
-      "s_cbranch_scc1 .Lvm_all%=\n\t"
-      "s_waitcnt vmcnt(%10)\n\t"
-      "s_branch .Lvm_done%=\n"
-      ".Lvm_all%=:\n\t"
-      "s_waitcnt vmcnt(%11)\n"
-      ".Lvm_done%=:"
-      : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
-        "+v"(v[7]), "+v"(pf)
-      : "s"(after_stores), "n"(N + NPF), "n"(NPF)
-      : "memory", "scc");
-}
-
-// 4 fp32 results -> storage type (round to nearest even; NaN stays NaN, overflow gives inf).
-// Global address space explicitly: a flat store would count in vmcnt out of order.
-// NT (compile time, so each instantiation holds ONE kind of store: an if / else of a
-// non-temporal and a plain store to one address is merged by the compiler into a plain store,
-// dropping the non-temporal hint -- that silently happened to every fp32 volume store in r02):
-//   true: non-temporal -- the volume is written once and never re-read by this kernel; plain
-//         stores allocate its lines in L2 and evict the feature lines the loads reuse
-//         (scripts/micro/mlp_patterns.hip: cfg2 reads + writes 140 us plain vs 106 us nt);
-//   false: plain -- fp32 rows with W % 4 != 0, whose 128-B row pieces straddle two lines: L2
-//         merges the two halves of a line before it writes the line back.
-template <bool NT, typename T>
-__device__ __forceinline__ void store_quad(T* p, f32x4v v) {
-  typedef __attribute__((address_space(1))) void gvoid;
-  gvoid* g = (gvoid*)p;
-  if constexpr (sizeof(T) == 4) {
-    if constexpr (SMCV_NT_STORE && NT)
-      __builtin_nontemporal_store(v, reinterpret_cast<__attribute__((address_space(1))) f32x4v*>(g));
-    else
-      *reinterpret_cast<__attribute__((address_space(1))) f32x4v*>(g) = v;
-  } else if constexpr (std::is_same<T, __half>::value) {
-    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-    const h4 r = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
-    if constexpr (SMCV_NT_STORE && NT)
-      __builtin_nontemporal_store(r, reinterpret_cast<__attribute__((address_space(1))) h4*>(g));
-    else
-      *reinterpret_cast<__attribute__((address_space(1))) h4*>(g) = r;
-  } else {
-    typedef __bf16 b4 __attribute__((ext_vector_type(4)));
-    const b4 r = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
-    if constexpr (SMCV_NT_STORE && NT)
-      __builtin_nontemporal_store(r, reinterpret_cast<__attribute__((address_space(1))) b4*>(g));
-    else
-      *reinterpret_cast<__attribute__((address_space(1))) b4*>(g) = r;
-  }
-}
-template <typename T>
-__device__ __forceinline__ void store_one(T* p, float v) {
-  typedef __attribute__((address_space(1))) void gvoid;
-  if constexpr (sizeof(T) == 4) {
-    *reinterpret_cast<__attribute__((address_space(1))) float*>((gvoid*)p) = v;
-  } else {
-    const T h = (T)v;
-    *reinterpret_cast<__attribute__((address_space(1))) unsigned short*>((gvoid*)p) =
-        __builtin_bit_cast(unsigned short, h);
-  }
-}
-
-template <typename T>
-__device__ __forceinline__ float ld1(const T* p) { return (float)*p; }
-
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-  return v;
-}
-
-// The fp32 split of two values x (channels 2q, 2q+1 of one pixel), scaled by sc = 2^k (exact):
-// h = rn16(x sc) and m = rn16(x sc - h), packed as (lo, hi) fp16 pairs.  Four v_fma_mix*, i.e.
-// two VALU per value (the compiler's cvt / cvt-back / subtract / pack sequence took four): the
-// mix forms evaluate x * sc - h exactly (x sc is exact, and h is its rounding, so the difference
-// is an fp32 number) and round it to fp16 once -- bit-identical to that sequence.
-__device__ __forceinline__ void split_pair(float a, float b, float sc, unsigned& h, unsigned& m) {
-  asm("v_fma_mixlo_f16 %0, %2, %4, 0\n\t"
-      "v_fma_mixhi_f16 %0, %3, %4, 0\n\t"
-      "v_fma_mixlo_f16 %1, %2, %4, -%0 op_sel_hi:[0,0,1]\n\t"
-      "v_fma_mixhi_f16 %1, %3, %4, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
-      : "=&v"(h), "=&v"(m)
-      : "v"(a), "v"(b), "v"(sc));
-}
-
-// exponent e with x = f 2^e, f in [0.5, 1) (x > 0 finite)
-__device__ __forceinline__ int exp_of(float x) { return __builtin_amdgcn_frexp_expf(x); }
 
 // Workgroups per CU: two (each wave owns 256 registers); the fused kernels too, since their
 // soft-argmin runs on the accumulators themselves before the shear.
@@ -759,7 +561,9 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
         }
       }
       // one block at a time (the live accumulators shrink block by block)
+#ifndef SMCV_EPI_FREE
       __builtin_amdgcn_sched_barrier(0);
+#endif
     }
   };
 
@@ -1058,12 +862,16 @@ int check_dot_args(const void* left, const void* right, const void* out, int dty
                    int64_t C, int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
                    const int64_t* r_strides, Strides4* ls, Strides4* rs);
 
+namespace h2band {
+int band_b16_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled);
+}
+
 namespace {
 // Shared validation; *vec = the shape takes the band kernels (4-pixel groups: W % 4 == 0,
 // 4-element aligned rows and feature pointers, a 16-B aligned output, channels > 0).
 int h2_prepare(const void* left, const void* right, const void* out, int dtype, int64_t N,
                int64_t C, int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
-               const int64_t* r_strides, h2band::Args* a, bool* vec) {
+               const int64_t* r_strides, h2band::Args* a, bool* vec, bool* al4 = nullptr) {
   Strides4 ls, rs;
   int rc = check_dot_args(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, &ls, &rs);
   if (rc) return rc;
@@ -1072,6 +880,7 @@ int h2_prepare(const void* left, const void* right, const void* out, int dtype, 
                        rs.n % 4 == 0 && rs.c % 4 == 0 && rs.h % 4 == 0 &&
                        ((reinterpret_cast<uintptr_t>(left) | reinterpret_cast<uintptr_t>(right)) % align == 0) &&
                        reinterpret_cast<uintptr_t>(out) % 16 == 0;
+  if (al4) *al4 = aligned4;
   // fp32 rows of any width (and any element strides): the 16-B feature loads and volume stores
   // are then only dword-aligned, which gfx950 global memory accesses allow (unaligned mode);
   // the row-end group is handled in load() / put() and the row-end quad in the epilogue
@@ -1110,12 +919,12 @@ int h2_prepare(const void* left, const void* right, const void* out, int dtype, 
 // *handled = false when the shape needs the generic path.
 int band_h2_entry(const void* left, const void* right, void* out, int dtype, int64_t N, int64_t C,
                   int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
-                  const int64_t* r_strides, int mode, void* stream, bool* handled) {
+                  const int64_t* r_strides, int mode, void* stream, bool* handled, bool allow_b16) {
   using namespace h2band;
   *handled = false;
   Args a;
-  bool vec = false;
-  int rc = h2_prepare(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, &a, &vec);
+  bool vec = false, al4 = false;
+  int rc = h2_prepare(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, &a, &vec, &al4);
   if (rc) return rc;
   if (!vec) return SM_OK;
   *handled = true;
@@ -1123,6 +932,11 @@ int band_h2_entry(const void* left, const void* right, void* out, int dtype, int
   const bool mean = mode == 1;
   a.mul = 1.0f / (float)C;
   hipStream_t st = as_stream(stream);
+  if (allow_b16 && dtype == SM_F32) {  // fp32, aligned rows: the four-waves-per-SIMD tiling
+    bool done = false;
+    rc = band_b16_run(a, N, mean, al4, st, &done);
+    if (done || rc != SM_OK) return rc;
+  }
   SM_DISPATCH_DTYPE(dtype, T0, {
     using T = typename std::conditional<std::is_same<T0, bf16_t>::value, __bf16, T0>::type;
     return by_tmax(a.pw, [&](auto tm) {

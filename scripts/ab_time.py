@@ -24,6 +24,10 @@ def ops():
         # name: (setup -> callable, pairs per launch, algorithmic bytes per pair)
         "cfg2": (lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192))(*feats((8, 64, 540, 960), torch.float32)),
                  8, 663552000),
+        "cfg2_h2": (lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="h2"))(*feats((8, 64, 540, 960), torch.float32)),
+                    8, 663552000),
+        "cfg2_b16": (lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="b16"))(*feats((8, 64, 540, 960), torch.float32)),
+                     8, 663552000),
         "cfg2_fused_nv": (lambda: (lambda L, R: lambda: F.inner_product_soft_argmin(L, R, 192, keep_volume=False))(
             *feats((8, 64, 540, 960), torch.float32)), 8, 267494400),
         "cfg2_regress": (lambda: (lambda v: lambda: F.soft_argmin(v))(torch.randn(8, 192, 540, 960, device="cuda")),

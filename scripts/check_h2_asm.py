@@ -7,7 +7,9 @@ kernel relies on two properties of the generated code, checked here for every in
      `s_waitcnt vmcnt` (a register copy there would read data that has not landed);
   2. no wave ends (s_endpgm) with such a load still in flight (the L2 touches included);
   3. no `flat_*` memory instruction exists (flat ops count in vmcnt out of order, which would
-     break the `vmcnt(4 (T-1))` wait that lets the output stores stay in flight).
+     break the `vmcnt(4 (T-1))` wait that lets the output stores stay in flight);
+  4. band_b16 (ip_b16.hip) has no scratch access at all: a spill reload counts in vmcnt and
+     would wait for the feature loads in flight.
 A may-pending dataflow over the kernel's basic blocks carries each load to every instruction it
 can reach before a vmcnt wait.
 
@@ -21,7 +23,8 @@ import sys
 import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = os.path.join(ROOT, "realtime_stereo_matcher_amd", "csrc", "ip_h2.hip")
+CSRC = os.path.join(ROOT, "realtime_stereo_matcher_amd", "csrc")
+SRCS = [os.path.join(CSRC, "ip_h2.hip"), os.path.join(CSRC, "ip_b16.hip")]
 
 
 def regs(tok):
@@ -38,7 +41,7 @@ def kernels(asm_text):
     only those loads are hand-counted (the compiler waits for its own)."""
     out, cur, in_asm = [], None, False
     for ln, line in enumerate(asm_text.splitlines(), 1):
-        if re.match(r"^_ZN4smcv6h2band7band_h2.*:", line):
+        if re.match(r"^_ZN4smcv6h2band(7band_h2|8band_b16).*:", line):
             cur = (line.split(":")[0], [])
             out.append(cur)
             continue
@@ -90,7 +93,7 @@ def blocks_of(body):
     return blocks, succ
 
 
-def transfer(block, pending, report=None):
+def transfer(block, pending, report=None, no_scratch=False):
     pending = set(pending)
     for ln, ins in block:
         hand = ins.startswith("@")  # from an inline-asm statement
@@ -104,6 +107,8 @@ def transfer(block, pending, report=None):
         if op == "s_endpgm" and pending and report is not None:
             report.append(f"{ln}: wave ends with loads in flight into v{sorted(pending)[:4]}...")
         toks = [t.strip(",") for t in ins.split()[1:]]
+        if no_scratch and op.startswith("scratch_") and report is not None:
+            report.append(f"{ln}: scratch access (a spill counts in vmcnt): {ins}")
         if hand and op in ("global_load_dwordx4", "global_load_dwordx2", "global_load_dword"):
             srcs = set()
             for t in toks[1:]:
@@ -135,33 +140,35 @@ def check(asm_text):
                         ins_state[j] |= out
                         changed = True
         rep = []
-        for i, b in enumerate(blocks):
-            transfer(b, ins_state[i], rep)
+        for i, b in enumerate(blocks):  # band_b16 must not spill at all (4 waves per SIMD)
+            transfer(b, ins_state[i], rep, no_scratch="8band_b16" in name)
         bad += [f"{name}:{r}" for r in rep]
     return bad
 
 
 def main():
     args = sys.argv[1:]
-    src = SRC
+    srcs = SRCS
     if "--stamps" in args:  # the diagnostic driver (scripts/ip_stamps.hip) instead
         args.remove("--stamps")
-        src = os.path.join(ROOT, "scripts", "ip_stamps.hip")
+        srcs = [os.path.join(ROOT, "scripts", "ip_stamps.hip")]
         args.append("-DSMCV_STAMPS")
-    stem = os.path.basename(src)[:-4]
-    with tempfile.TemporaryDirectory() as td:
-        cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", *args, "-I",
-               os.path.join(ROOT, "include"), "-c", src, "--save-temps", "-o",
-               os.path.join(td, "h2.o")]
-        subprocess.run(cmd, cwd=td, check=True, capture_output=True)
-        asm = open(os.path.join(td, f"{stem}-hip-amdgcn-amd-amdhsa-gfx950.s")).read()
-    bad = check(asm)
+    bad, n = [], 0
+    for src in srcs:
+        stem = os.path.basename(src)[:-4]
+        with tempfile.TemporaryDirectory() as td:
+            cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++20", "--offload-arch=gfx950", *args, "-I",
+                   os.path.join(ROOT, "include"), "-c", src, "--save-temps", "-o",
+                   os.path.join(td, "h2.o")]
+            subprocess.run(cmd, cwd=td, check=True, capture_output=True)
+            asm = open(os.path.join(td, f"{stem}-hip-amdgcn-amd-amdhsa-gfx950.s")).read()
+        bad += check(asm)
+        n += len(kernels(asm))
     for b in bad[:40]:
         print(b)
-    n = len(kernels(asm))
     print(f"{n} kernels checked, {len(bad)} problems")
     if n == 0:
-        print("no band_h2 kernels found in the asm (renamed?)")
+        print("no band kernels found in the asm (renamed?)")
         return 1
     return 1 if bad else 0
 
