@@ -15,7 +15,7 @@ int band_f32_entry(const void* left, const void* right, void* out, int dtype, in
 int band_h2_entry(const void* left, const void* right, void* out, int dtype, int64_t N, int64_t C,
                   int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
                   const int64_t* r_strides, int mode, void* stream, bool* handled,
-                  bool allow_b16);
+                  int variant);
 int band_h2_groupwise_entry(const void* left, const void* right, float* out, int dtype, int64_t N,
                             int64_t C, int64_t H, int64_t W, int64_t D, int64_t G,
                             const int64_t* l_strides, const int64_t* r_strides, void* stream,
@@ -70,10 +70,13 @@ extern "C" int sm_cv_inner_product_ex(const void* left, const void* right, void*
     }
     case SM_IP_AUTO:  // the two-plane fp16 band kernel; odd shapes: the exact VALU kernel
     case SM_IP_MFMA_H2:
-    case SM_IP_MFMA_B16: {
+    case SM_IP_MFMA_B16:
+    case SM_IP_MFMA_H2DB: {
       bool handled = false;
+      // AUTO: fp32 aligned rows take the double-buffered band (band_h2db), the rest band_h2
+      const int variant = algo == SM_IP_MFMA_B16 ? 1 : (algo == SM_IP_MFMA_H2DB || algo == SM_IP_AUTO) ? 2 : 0;
       int rc = band_h2_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
-                             stream, &handled, algo == SM_IP_MFMA_B16);
+                             stream, &handled, variant);
       if (handled || rc != SM_OK) return rc;
       return dot_volume_valu_entry(left, right, out, dtype, N, C, H, W, D, 1, l_strides,
                                    r_strides, 0, stream);
@@ -104,7 +107,7 @@ extern "C" int sm_cv_correlation_mean(const void* left, const void* right, void*
   SM_ENTRY_BEGIN
   bool handled = false;
   int rc = band_h2_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 1, stream,
-                         &handled, false);
+                         &handled, 2);
   if (handled || rc != SM_OK) return rc;
   return dot_volume_valu_entry(left, right, out, dtype, N, C, H, W, D, 1, l_strides, r_strides,
                                1, stream);

@@ -48,6 +48,10 @@
 // same pass -- with or without the volume.
 #include "band_common.h"
 
+#ifndef SMCV_STORE_THROTTLE
+#define SMCV_STORE_THROTTLE 0
+#endif
+
 namespace smcv {
 namespace h2band {
 
@@ -449,15 +453,22 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
       fuse_regs(k, scale, xlt);
       if (FUSE == 2 || !store_vol) return;  // the volume-free pass: no shear, no ring, no stores
     }
-#pragma unroll
-    for (int t = TMAX - 1; t >= 0; --t) {
-      const int a = TMAX - 2 - t;
+    // Block t writes its 16 cells into the ring (chunks a and a+1, a = T-2-t); chunk a is then
+    // complete and is read back (4 x 16 B per lane) and stored.  Software-pipelined (PIPE): the
+    // readout of chunk a is consumed only after block t-1's ring writes are issued, so its LDS
+    // latency hides behind them instead of stalling the wave once per block (the 3-slot ring
+    // keeps chunk a's slot apart from the chunks block t-1 writes, and a wave's LDS operations
+    // execute in order anyway).
+    constexpr bool PIPE = FUSE == 0;
+    auto write_block = [&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      constexpr int a = TMAX - 2 - t;
       // per block, opaque to the compiler: the per-element addresses and selects below are
       // recomputed in each block (two VALU each) instead of being hoisted out of the block loop
       // as 16+ loop-invariant registers (which spill at two workgroups per CU)
-      unsigned wb = wbase, rb = rdbase;
-      int uu = u, jl = jlane, ls_ = lane_st, rlo = rl, clo = cl;
-      asm volatile("" : "+v"(wb), "+v"(uu), "+v"(jl), "+v"(rb), "+v"(ls_), "+v"(rlo), "+v"(clo));
+      unsigned wb = wbase;
+      int uu = u, jl = jlane;
+      asm volatile("" : "+v"(wb), "+v"(uu), "+v"(jl));
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int ci = (i & 3) + 8 * (i >> 2);
@@ -492,79 +503,106 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
       }
       // the wave's own ring writes precede its reads (LDS executes a wave's operations in order)
       asm volatile("" ::: "memory");
-      if (a >= 0) {
-        f32x4v v[4];
+    };
+    auto read_chunk = [&](auto tc, f32x4v (&v)[4]) {
+      constexpr int t = decltype(tc)::value;
+      constexpr int a = TMAX - 2 - t;
+      unsigned rb = rdbase;
+      asm volatile("" : "+v"(rb));
 #pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-          const unsigned ra = LAYOUT == kNDHW ? rb + (unsigned)((a % 3) * kSlot + 8 * qq * 128)
-                                              : rb + (unsigned)(8 * qq * 384 + (a % 3) * 128);
-          if constexpr ((SMCV_ABLATE & 32) != 0)
-            v[qq] = f32x4v{acc[t][4 * qq], acc[t][4 * qq + 1], acc[t][4 * qq + 2], acc[t][4 * qq + 3]};
-          else
-            v[qq] = lds_load4(ra);
-        }
-
-        if (store_vol) {
-          if constexpr (LAYOUT == kNDHW) {
-            TO* ol = out + (((size_t)k.n * D + k.dp + 32 * a) * plane_stride +
-                            (size_t)k.y * W + x0w) + ls_;
-            // rows 8 apart: one uniform stride, the pointer stepped store by store (kept
-            // opaque, so no 64-bit per-row offsets are hoisted into registers)
-            const size_t st8 = (size_t)8 * plane_stride;
-            if (fast) {  // every store valid: exactly 4 (T-1) per lane, counted by vm_wait
+      for (int qq = 0; qq < 4; ++qq) {
+        const unsigned ra = LAYOUT == kNDHW ? rb + (unsigned)((a % 3) * kSlot + 8 * qq * 128)
+                                            : rb + (unsigned)(8 * qq * 384 + (a % 3) * 128);
+        if constexpr ((SMCV_ABLATE & 32) != 0)
+          v[qq] = f32x4v{acc[t][4 * qq], acc[t][4 * qq + 1], acc[t][4 * qq + 2], acc[t][4 * qq + 3]};
+        else
+          v[qq] = lds_load4(ra);
+      }
+    };
+    auto store_chunk = [&](int a, const f32x4v (&v)[4]) {
+      if (!store_vol) return;
+      int ls_ = lane_st, rlo = rl, clo = cl;
+      asm volatile("" : "+v"(ls_), "+v"(rlo), "+v"(clo));
+      if constexpr (LAYOUT == kNDHW) {
+        TO* ol = out + (((size_t)k.n * D + k.dp + 32 * a) * plane_stride +
+                        (size_t)k.y * W + x0w) + ls_;
+        // rows 8 apart: one uniform stride, the pointer stepped store by store (kept
+        // opaque, so no 64-bit per-row offsets are hoisted into registers)
+        const size_t st8 = (size_t)8 * plane_stride;
+        if (fast) {  // every store valid: exactly 4 (T-1) per lane, counted by vm_wait
 #pragma unroll
-              for (int qq = 0; qq < 4; ++qq) {
-                asm volatile("" : "+v"(ol));
+          for (int qq = 0; qq < 4; ++qq) {
+            asm volatile("" : "+v"(ol));
+            store_quad<NTQ>(ol, v[qq]);
+            ol += st8;
+          }
+        } else {
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            asm volatile("" : "+v"(ol));
+            const int dl = 32 * a + 8 * qq + rlo;
+            const int xq = x0w + 4 * clo;
+            if (dl < k.Dp && xq < W && !(SMCV_ABLATE & 4)) {
+              if (xq + 4 <= W) {
                 store_quad<NTQ>(ol, v[qq]);
-                ol += st8;
-              }
-            } else {
+              } else {  // the row's last, partial quad (W % 4 != 0)
 #pragma unroll
-              for (int qq = 0; qq < 4; ++qq) {
-                asm volatile("" : "+v"(ol));
-                const int dl = 32 * a + 8 * qq + rlo;
-                const int xq = x0w + 4 * clo;
-                if (dl < k.Dp && xq < W && !(SMCV_ABLATE & 4)) {
-                  if (xq + 4 <= W) {
-                    store_quad<NTQ>(ol, v[qq]);
-                  } else {  // the row's last, partial quad (W % 4 != 0)
-#pragma unroll
-                    for (int e = 0; e < 3; ++e)
-                      if (xq + e < W) store_one<TO>(ol + e, v[qq][e]);
-                  }
-                }
-                ol += st8;
+                for (int e = 0; e < 3; ++e)
+                  if (xq + e < W) store_one<TO>(ol + e, v[qq][e]);
               }
             }
-          } else {
-            const size_t pix = (((size_t)k.n * args.G + k.g) * H + k.y) * (size_t)W + x0w;
-            TO* ol = out + (pix * (size_t)D + k.dp + 32 * a) + ls_;
-            asm volatile("" : "+v"(ol));
-            if (fast) {
+            ol += st8;
+          }
+        }
+      } else {
+        const size_t pix = (((size_t)k.n * args.G + k.g) * H + k.y) * (size_t)W + x0w;
+        TO* ol = out + (pix * (size_t)D + k.dp + 32 * a) + ls_;
+        asm volatile("" : "+v"(ol));
+        if (fast) {
 #pragma unroll
-              for (int qq = 0; qq < 4; ++qq) store_quad<true>(ol + (size_t)(8 * qq) * D, v[qq]);
+          for (int qq = 0; qq < 4; ++qq) store_quad<true>(ol + (size_t)(8 * qq) * D, v[qq]);
+        } else {
+          const int d0 = 32 * a + 4 * clo;
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            if (x0w + 8 * qq + rlo >= W || (SMCV_ABLATE & 4)) continue;
+            if (d0 + 4 <= k.Dp && dq) {
+              store_quad<true>(ol + (size_t)(8 * qq) * D, v[qq]);
             } else {
-              const int d0 = 32 * a + 4 * clo;
 #pragma unroll
-              for (int qq = 0; qq < 4; ++qq) {
-                if (x0w + 8 * qq + rlo >= W || (SMCV_ABLATE & 4)) continue;
-                if (d0 + 4 <= k.Dp && dq) {
-                  store_quad<true>(ol + (size_t)(8 * qq) * D, v[qq]);
-                } else {
-#pragma unroll
-                  for (int e = 0; e < 4; ++e)
-                    if (d0 + e < k.Dp) store_one<TO>(ol + (size_t)(8 * qq) * D + e, v[qq][e]);
-                }
-              }
+              for (int e = 0; e < 4; ++e)
+                if (d0 + e < k.Dp) store_one<TO>(ol + (size_t)(8 * qq) * D + e, v[qq][e]);
             }
           }
         }
       }
-      // one block at a time (the live accumulators shrink block by block)
-#ifndef SMCV_EPI_FREE
-      __builtin_amdgcn_sched_barrier(0);
+    };
+    f32x4v vp[4];  // the readout of the previous block's chunk (PIPE)
+    [&]<int... I_>(std::integer_sequence<int, I_...>) {
+      (
+          [&] {
+            constexpr int t = TMAX - 1 - I_;
+            constexpr int a = TMAX - 2 - t;
+            write_block(std::integral_constant<int, t>{});
+            if constexpr (PIPE) {
+#if SMCV_STORE_THROTTLE
+              // at most SMCV_STORE_THROTTLE of this wave's stores in flight (the feature loads,
+              // older, complete first): experiment
+              if constexpr (a >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SMCV_STORE_THROTTLE) : "memory");
 #endif
-    }
+              if constexpr (a >= 1) store_chunk(a - 1, vp);
+              if constexpr (a >= 0) read_chunk(std::integral_constant<int, t>{}, vp);
+            } else if constexpr (a >= 0) {
+              f32x4v v[4];
+              read_chunk(std::integral_constant<int, t>{}, v);
+              store_chunk(a, v);
+            }
+            // one block at a time (the live accumulators shrink block by block)
+            __builtin_amdgcn_sched_barrier(0);
+          }(),
+          ...);
+    }(std::make_integer_sequence<int, TMAX>{});
+    if constexpr (PIPE && TMAX >= 2) store_chunk(TMAX - 2, vp);
   };
 
   auto epilogue_n = [&](const Work& k, bool fast, auto ntc) {
@@ -864,6 +902,7 @@ int check_dot_args(const void* left, const void* right, const void* out, int dty
 
 namespace h2band {
 int band_b16_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled);
+int band_h2db_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled);
 }
 
 namespace {
@@ -919,7 +958,7 @@ int h2_prepare(const void* left, const void* right, const void* out, int dtype, 
 // *handled = false when the shape needs the generic path.
 int band_h2_entry(const void* left, const void* right, void* out, int dtype, int64_t N, int64_t C,
                   int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
-                  const int64_t* r_strides, int mode, void* stream, bool* handled, bool allow_b16) {
+                  const int64_t* r_strides, int mode, void* stream, bool* handled, int variant) {
   using namespace h2band;
   *handled = false;
   Args a;
@@ -932,9 +971,12 @@ int band_h2_entry(const void* left, const void* right, void* out, int dtype, int
   const bool mean = mode == 1;
   a.mul = 1.0f / (float)C;
   hipStream_t st = as_stream(stream);
-  if (allow_b16 && dtype == SM_F32) {  // fp32, aligned rows: the four-waves-per-SIMD tiling
+  // fp32 with aligned rows: variant 1 the four-waves-per-SIMD tiling (band_b16), variant 2 the
+  // double-buffered pipeline (band_h2db); other shapes (and variant 0) run band_h2
+  if (variant != 0 && dtype == SM_F32) {
     bool done = false;
-    rc = band_b16_run(a, N, mean, al4, st, &done);
+    rc = variant == 1 ? band_b16_run(a, N, mean, al4, st, &done)
+                      : band_h2db_run(a, N, mean, al4, st, &done);
     if (done || rc != SM_OK) return rc;
   }
   SM_DISPATCH_DTYPE(dtype, T0, {

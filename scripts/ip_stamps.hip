@@ -8,6 +8,7 @@
 #include "../realtime_stereo_matcher_amd/csrc/ip_f32.hip"
 #include "../realtime_stereo_matcher_amd/csrc/ip_h2.hip"
 #include "../realtime_stereo_matcher_amd/csrc/ip_b16.hip"
+#include "../realtime_stereo_matcher_amd/csrc/ip_h2db.hip"
 
 #ifdef SMCV_STAMPS
 namespace smcv {
@@ -37,13 +38,13 @@ int main(int argc, char** argv) {
   hipMalloc(&O, nout * 4);
   hipMalloc(&disp, N * H * W * 4);
   const bool f32 = !strcmp(mode, "f32");
-  const bool b16 = !strcmp(mode, "b16");
-  const bool h2 = !strcmp(mode, "h2") || b16;
+  const bool b16 = !strcmp(mode, "b16"), db = !strcmp(mode, "h2db");
+  const bool h2 = !strcmp(mode, "h2") || b16 || db;
   const bool fused = !strcmp(mode, "fused"), fusednv = !strcmp(mode, "fusednv");
   const bool band = h2 || fused || fusednv || gw;
   bool handled = false;
   auto run = [&]() {
-    if (h2) return smcv::band_h2_entry(L, R, O, SM_F32, N, C, H, W, D, nullptr, nullptr, 0, nullptr, &handled, b16);
+    if (h2) return smcv::band_h2_entry(L, R, O, SM_F32, N, C, H, W, D, nullptr, nullptr, 0, nullptr, &handled, b16 ? 1 : db ? 2 : 0);
     if (fused || fusednv)
       return smcv::band_h2_fused_entry(L, R, fused ? O : nullptr, disp, SM_F32, N, C, H, W, D, nullptr,
                                        nullptr, 0, nullptr, &handled, nullptr, 0);
