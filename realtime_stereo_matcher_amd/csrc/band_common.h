@@ -213,5 +213,42 @@ __device__ __forceinline__ void split_pair(float a, float b, float sc, unsigned&
 // exponent e with x = f 2^e, f in [0.5, 1) (x > 0 finite)
 __device__ __forceinline__ int exp_of(float x) { return __builtin_amdgcn_frexp_expf(x); }
 
+// The persistent grid's schedule (band_h2, band_h2db, band_b16).  Workgroups b and b+8 share an
+// XCD, and each XCD group walks a contiguous range of row segments, so neighbouring segments of
+// a row run on one XCD at the same time and share its L2 for the right window.  Item i of a
+// workgroup is segment j = gi + (i / npass) gsz of its group's range, pass i % npass: the D
+// passes of a segment are consecutive items of one workgroup, so the second pass's feature
+// loads find the lines the first one fetched in L2 (concurrent passes on different workgroups
+// drift apart and miss: cfg4 fetched its features 1.95x in round 2).  With gsz % 8 == 0 every
+// workgroup would keep one tile index (j % 8) for the whole launch, so the workgroups of the
+// 64-pixel last tile of a 960-pixel row would idle half the time; rotating each complete
+// aligned 8-segment block by the round spreads the short tiles over all workgroups (the set
+// of segments in flight per round, and so the L2 sharing, is unchanged).
+struct Sched {
+  int gi, gsz, sbeg, scnt, nitems, npass;
+  bool rot, none;
+  __device__ __forceinline__ Sched(int nwork, int np) {
+    const int grp = blockIdx.x & 7;
+    gi = blockIdx.x >> 3;
+    gsz = gridDim.x >> 3;
+    npass = np;
+    const int nseg = nwork / np;
+    const int q = nseg >> 3, rr = nseg & 7;
+    sbeg = grp < rr ? grp * (q + 1) : rr * (q + 1) + (grp - rr) * q;
+    scnt = q + (grp < rr ? 1 : 0);
+    none = gi >= scnt;  // the whole workgroup leaves together
+    nitems = none ? 0 : ((scnt - gi + gsz - 1) / gsz) * np;
+    rot = (gsz & 7) == 0;
+  }
+  __device__ __forceinline__ int item(int i) const {
+    const int si = npass == 1 ? i : i / npass;
+    const int p = i - si * npass;
+    const int j = gi + si * gsz;
+    const int b = j & ~7;
+    const int seg = sbeg + ((rot && b + 8 <= scnt) ? (b | ((j + si) & 7)) : j);
+    return seg * npass + p;
+  }
+};
+
 }  // namespace h2band
 }  // namespace smcv

@@ -90,23 +90,11 @@ __global__ __launch_bounds__(bThreads, 4) void band_b16(Args args) {
   const int cpg = args.cpg, H = args.H, W = args.W, D = args.D;
   const Strides4 ls = args.ls, rs = args.rs;
 
-  // work range of this workgroup's XCD group, rotated as in band_h2 (consecutive segments of a
-  // row run on one XCD at the same time and share its L2 for the right window)
-  const int grp = blockIdx.x & 7;
-  const int gi = blockIdx.x >> 3;
-  const int gsz = gridDim.x >> 3;
-  const int q = args.nwork >> 3, rr = args.nwork & 7;
-  const int wbeg = grp < rr ? grp * (q + 1) : rr * (q + 1) + (grp - rr) * q;
-  const int wend = wbeg + q + (grp < rr ? 1 : 0);
-  if (wbeg + gi >= wend) return;  // the whole workgroup leaves together
-  const int nitems = (wend - (wbeg + gi) + gsz - 1) / gsz;
-  const int wcnt = wend - wbeg;
-  const bool rot = (gsz & 7) == 0;
-  auto witem = [&](int i) -> int {
-    const int j = gi + i * gsz;
-    const int b = j & ~7;
-    return wbeg + ((rot && b + 8 <= wcnt) ? (b | ((j + i) & 7)) : j);
-  };
+  // the persistent schedule: XCD-grouped segment ranges, D passes consecutive (Sched)
+  const Sched sched(args.nwork, args.npass);
+  if (sched.none) return;  // the whole workgroup leaves together
+  const int nitems = sched.nitems;
+  auto witem = [&](int i) -> int { return sched.item(i); };
   const int nks = (cpg + bKC - 1) / bKC;
 
   const int tid = threadIdx.x;

@@ -111,28 +111,11 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
   const int cpg = args.cpg, H = args.H, W = args.W, D = args.D;
   const Strides4 ls = args.ls, rs = args.rs;
 
-  // work range of this workgroup's XCD group (blocks b and b+8 share an XCD): consecutive
-  // segments of a row run on one XCD at the same time and share its L2 for the right window
-  const int grp = blockIdx.x & 7;
-  const int gi = blockIdx.x >> 3;
-  const int gsz = gridDim.x >> 3;
-  const int q = args.nwork >> 3, rr = args.nwork & 7;
-  const int wbeg = grp < rr ? grp * (q + 1) : rr * (q + 1) + (grp - rr) * q;
-  const int wend = wbeg + q + (grp < rr ? 1 : 0);
-  if (wbeg + gi >= wend) return;  // the whole workgroup leaves together
-  const int nitems = (wend - (wbeg + gi) + gsz - 1) / gsz;
-  // item i of this workgroup is group-local index j = gi + i gsz.  With gsz % 8 == 0 every
-  // workgroup would keep one tile index (j % 8) for the whole launch, so the workgroups of the
-  // 64-pixel last tile of a 960-pixel row would idle half the time; rotating each complete
-  // aligned 8-item block by the round i = j / gsz spreads the short tiles over all workgroups.
-  // The set of items in flight per round (and so the L2 sharing) is unchanged.
-  const int wcnt = wend - wbeg;
-  const bool rot = (gsz & 7) == 0;
-  auto witem = [&](int i) -> int {
-    const int j = gi + i * gsz;
-    const int b = j & ~7;
-    return wbeg + ((rot && b + 8 <= wcnt) ? (b | ((j + i) & 7)) : j);
-  };
+  // the persistent schedule: XCD-grouped segment ranges, D passes consecutive (Sched)
+  const Sched sched(args.nwork, args.npass);
+  if (sched.none) return;  // the whole workgroup leaves together
+  const int nitems = sched.nitems;
+  auto witem = [&](int i) -> int { return sched.item(i); };
   const int nks = (cpg + kKC - 1) / kKC;
   const bool store_vol = FUSE != 2 && __builtin_amdgcn_readfirstlane(args.out != nullptr ? 1 : 0) != 0;
   // NGHWD quads are 16-B aligned only when D % 4 == 0

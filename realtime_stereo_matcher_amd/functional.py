@@ -33,6 +33,17 @@ _ALGOS = {"auto": _lib.SM_IP_AUTO, "valu": _lib.SM_IP_VALU, "mfma": _lib.SM_IP_M
 
 
 # ----------------------------------------------------------------------------------- plumbing
+def _traced():
+    """Under torch.jit.trace or a compiler the call is routed through torch.ops.stereocv, so the
+    traced graph holds the operator instead of its output as a constant (library.py)."""
+    from . import library
+    return library.tracing()
+
+
+def _ops():
+    from . import library  # noqa: F401  (registers the ops)
+    return torch.ops.stereocv
+
 def _device_check(*ts):
     dev = ts[0].device
     for t in ts:
@@ -140,6 +151,8 @@ def _autocast_fp32(*ts):
 # ----------------------------------------------------------------------------- a-1, a-6, a-2
 def inner_product_volume(left, right, max_disparity, algo="auto"):
     """(N,C,H,W) x2 -> (N,D,H,W): sum_c L*R(x-d) for x >= d, 0 elsewhere (left dtype/device)."""
+    if _traced():
+        return _ops().inner_product_volume(left, right, int(max_disparity), algo)
     left, right, dev, code = _pair(left, right, "inner_product_volume")
     D = _disp(max_disparity, "inner_product_volume")
     if algo not in _ALGOS:
@@ -161,6 +174,8 @@ def inner_product_volume(left, right, max_disparity, algo="auto"):
 
 def correlation_volume(l_fmap, r_fmap, max_disp):
     """(N,C,H,W) x2 -> (N,D,H,W): mean_c L*R(x-d) for x >= d, 0 elsewhere."""
+    if _traced():
+        return _ops().correlation_volume(l_fmap, r_fmap, int(max_disp))
     left, right, dev, code = _pair(l_fmap, r_fmap, "correlation_volume")
     D = _disp(max_disp, "correlation_volume")
     n, c, h, w = left.shape
@@ -236,6 +251,8 @@ def groupwise_volume(left, right, n_groups, max_disparity):
     Deviation (documented): the reference allocates its output on the CPU regardless of the
     input device (cost_volume/groupwise.py:39); this engine returns it on the input device.
     """
+    if _traced():
+        return _ops().groupwise_volume(left, right, int(n_groups), int(max_disparity))
     G = int(n_groups)
     D = _disp(max_disparity, "groupwise_volume")
     if isinstance(left, torch.Tensor) and left.dim() == 4 and D > 0:
@@ -261,6 +278,8 @@ def groupwise_volume(left, right, n_groups, max_disparity):
 # ----------------------------------------------------------------------------- a-3, a-4, a-5
 def concat_volume(left, right, max_disparity):
     """(N,C,H,W) x2 -> (N,2C,H,W,D): [:C]=L, [C:]=R(x-d) for x >= d, 0 elsewhere (bit-exact)."""
+    if _traced():
+        return _ops().concat_volume(left, right, int(max_disparity))
     left, right, dev, code = _pair(left, right, "concat_volume")
     D = _disp(max_disparity, "concat_volume")
     n, c, h, w = left.shape
@@ -279,6 +298,8 @@ def concat_volume(left, right, max_disparity):
 
 def interweave(left, right):
     """(N,C,H,W) x2 -> (N,2C,H,W): even channels L, odd channels R (bit-exact)."""
+    if _traced():
+        return _ops().interweave(left, right)
     left, right, dev, code = _pair(left, right, "interweave")
     n, c, h, w = left.shape
 
@@ -296,6 +317,8 @@ def interweave(left, right):
 
 def interweave_volume(left, right, max_disparity):
     """(N,C,H,W) x2 -> (N,2C,D,H,W): the v4 per-disparity interweave, 0 for x < d (bit-exact)."""
+    if _traced():
+        return _ops().interweave_volume(left, right, int(max_disparity))
     left, right, dev, code = _pair(left, right, "interweave_volume")
     D = _disp(max_disparity, "interweave_volume")
     n, c, h, w = left.shape
@@ -346,6 +369,8 @@ def v4_volume(featL, featR, w1, b1, w2, b2, w3, b3, w4, b4, volume_size=48):
 
 def difference_volume(left, right, max_disp):
     """(N,C,H,W) x2 -> (N,C,D,H,W): L - R(x-d) for x >= d, 1.0 elsewhere (bit-exact)."""
+    if _traced():
+        return _ops().difference_volume(left, right, int(max_disp))
     left, right, dev, code = _pair(left, right, "difference_volume")
     D = _disp(max_disp, "difference_volume")
     n, c, h, w = left.shape
@@ -397,6 +422,9 @@ def soft_argmin(volume, keepdim=True):
     """sum_d d * softmax_d(volume) -> (N,1,H,W) (keepdim) or (N,H,W); fp64 accumulation.
     The output has the volume's dtype; under torch autocast an fp16 / bf16 volume gives fp32
     (the reference's autocast F.softmax + torch.sum)."""
+    if _traced():
+        out = _ops().soft_argmin(volume)
+        return out.unsqueeze(1) if keepdim else out
     out = _regress(volume, _lib.SM_REGRESS_SOFTMAX, "soft_argmin")
     return out.unsqueeze(1) if keepdim else out
 
@@ -404,6 +432,8 @@ def soft_argmin(volume, keepdim=True):
 def regression_presoftmax(prob):
     """sum_d d * prob[:, d] over an already-softmaxed (N,D,H,W) volume -> (N,H,W) (fp32 under
     autocast for an fp16 / bf16 input, the reference's autocast torch.sum)."""
+    if _traced():
+        return _ops().regression_presoftmax(prob)
     return _regress(prob, _lib.SM_REGRESS_PRESOFTMAXED, "regression_presoftmax")
 
 
@@ -422,11 +452,15 @@ def _argext(volume, mode, what):
 
 def hard_argmin(volume):
     """First index of the minimum over D -> (N,H,W) int64 (ties -> lowest d, NaN wins)."""
+    if _traced():
+        return _ops().hard_argmin(volume)
     return _argext(volume, _lib.SM_ARGMIN, "hard_argmin")
 
 
 def hard_argmax(volume):
     """First index of the maximum over D -> (N,H,W) int64 (ties -> lowest d, NaN wins)."""
+    if _traced():
+        return _ops().hard_argmax(volume)
     return _argext(volume, _lib.SM_ARGMAX, "hard_argmax")
 
 

@@ -1,0 +1,189 @@
+"""The engine's operators as PyTorch custom ops (``torch.ops.stereocv.*``) with fake kernels.
+
+The reference networks are traced by ``torch.onnx.export`` (tools/convert.py:18-26) and by
+thop / fvcore (tools/profiler.py:11-26).  A ctypes call is opaque to a tracer: ``torch.jit.trace``
+would bake the call's output in as a constant and ``torch.export`` / ``torch.compile`` could
+not see through it.  Registered here with ``torch.library.custom_op``, each operator is one node
+of the traced graph: ``functional`` routes a call through ``torch.ops.stereocv.<name>`` whenever
+it runs under ``torch.jit.trace`` or a compiler (dynamo / export), the fake kernel gives
+FakeTensor tracing the output's shape, dtype and device, and the real kernel is the same
+libstereocv call as the eager path (no CPU fallback).  The ops are forward-only like the rest
+of the engine: their backward raises ``NotImplementedError``.
+"""
+from __future__ import annotations
+
+import threading
+
+import torch
+
+from . import functional as F
+
+_state = threading.local()
+
+
+def tracing() -> bool:
+    """True when a functional call should go through torch.ops.stereocv (a tracer or compiler
+    is recording, and the call is not already the body of one of these ops)."""
+    if getattr(_state, "inside", False):
+        return False
+    try:
+        compiling = torch.compiler.is_compiling()
+    except AttributeError:  # older torch
+        compiling = False
+    return torch.jit.is_tracing() or compiling
+
+
+class _Inside:
+    def __enter__(self):
+        self.prev = getattr(_state, "inside", False)
+        _state.inside = True
+
+    def __exit__(self, *exc):
+        _state.inside = self.prev
+
+
+def _forward_only(ctx, *grads):
+    raise NotImplementedError(
+        "realtime_stereo_matcher_amd cost-volume kernels are forward/inference-only; "
+        "backward is not implemented")
+
+
+def _no_ctx(ctx, inputs, output):
+    return None
+
+
+def _register(name, impl, fake):
+    op = torch.library.custom_op(f"stereocv::{name}", mutates_args=())(impl)
+    op.register_fake(fake)
+    torch.library.register_autograd(f"stereocv::{name}", _forward_only, setup_context=_no_ctx)
+    return op
+
+
+def _empty(shape, like, dtype=None):
+    return like.new_empty(shape, dtype=dtype if dtype is not None else like.dtype)
+
+
+# ------------------------------------------------------------------------------------- ops
+def _inner_product(left: torch.Tensor, right: torch.Tensor, max_disparity: int,
+                   algo: str) -> torch.Tensor:
+    with _Inside():
+        return F.inner_product_volume(left, right, max_disparity, algo=algo)
+
+
+def _inner_product_fake(left, right, max_disparity, algo):
+    n, _, h, w = left.shape
+    return _empty((n, max_disparity, h, w), left)
+
+
+def _correlation(left: torch.Tensor, right: torch.Tensor, max_disp: int) -> torch.Tensor:
+    with _Inside():
+        return F.correlation_volume(left, right, max_disp)
+
+
+def _correlation_fake(left, right, max_disp):
+    n, _, h, w = left.shape
+    return _empty((n, max_disp, h, w), left)
+
+
+def _groupwise(left: torch.Tensor, right: torch.Tensor, n_groups: int,
+               max_disparity: int) -> torch.Tensor:
+    with _Inside():
+        return F.groupwise_volume(left, right, n_groups, max_disparity)
+
+
+def _groupwise_fake(left, right, n_groups, max_disparity):
+    n, _, h, w = left.shape
+    return _empty((n, n_groups, h, w, max_disparity), left, torch.float32)
+
+
+def _concat(left: torch.Tensor, right: torch.Tensor, max_disparity: int) -> torch.Tensor:
+    with _Inside():
+        return F.concat_volume(left, right, max_disparity)
+
+
+def _concat_fake(left, right, max_disparity):
+    n, c, h, w = left.shape
+    return _empty((n, 2 * c, h, w, max_disparity), left)
+
+
+def _interweave(left: torch.Tensor, right: torch.Tensor) -> torch.Tensor:
+    with _Inside():
+        return F.interweave(left, right)
+
+
+def _interweave_fake(left, right):
+    n, c, h, w = left.shape
+    return _empty((n, 2 * c, h, w), left)
+
+
+def _interweave_volume(left: torch.Tensor, right: torch.Tensor, max_disparity: int) -> torch.Tensor:
+    with _Inside():
+        return F.interweave_volume(left, right, max_disparity)
+
+
+def _interweave_volume_fake(left, right, max_disparity):
+    n, c, h, w = left.shape
+    return _empty((n, 2 * c, max_disparity, h, w), left)
+
+
+def _difference(left: torch.Tensor, right: torch.Tensor, max_disp: int) -> torch.Tensor:
+    with _Inside():
+        return F.difference_volume(left, right, max_disp)
+
+
+def _difference_fake(left, right, max_disp):
+    n, c, h, w = left.shape
+    return _empty((n, c, max_disp, h, w), left)
+
+
+def _regress_dtype(volume):
+    # the autocast rule of functional._regress: fp32 from a half volume under autocast
+    return torch.float32 if F._autocast_fp32(volume) else volume.dtype
+
+
+def _soft_argmin(volume: torch.Tensor) -> torch.Tensor:
+    with _Inside():
+        return F.soft_argmin(volume, keepdim=False)
+
+
+def _soft_argmin_fake(volume):
+    n, _, h, w = volume.shape
+    return _empty((n, h, w), volume, _regress_dtype(volume))
+
+
+def _presoftmax(prob: torch.Tensor) -> torch.Tensor:
+    with _Inside():
+        return F.regression_presoftmax(prob)
+
+
+def _presoftmax_fake(prob):
+    n, _, h, w = prob.shape
+    return _empty((n, h, w), prob, _regress_dtype(prob))
+
+
+def _argext_fake(volume):
+    n, _, h, w = volume.shape
+    return _empty((n, h, w), volume, torch.int64)
+
+
+def _hard_argmin(volume: torch.Tensor) -> torch.Tensor:
+    with _Inside():
+        return F.hard_argmin(volume)
+
+
+def _hard_argmax(volume: torch.Tensor) -> torch.Tensor:
+    with _Inside():
+        return F.hard_argmax(volume)
+
+
+inner_product_volume = _register("inner_product_volume", _inner_product, _inner_product_fake)
+correlation_volume = _register("correlation_volume", _correlation, _correlation_fake)
+groupwise_volume = _register("groupwise_volume", _groupwise, _groupwise_fake)
+concat_volume = _register("concat_volume", _concat, _concat_fake)
+interweave = _register("interweave", _interweave, _interweave_fake)
+interweave_volume = _register("interweave_volume", _interweave_volume, _interweave_volume_fake)
+difference_volume = _register("difference_volume", _difference, _difference_fake)
+soft_argmin = _register("soft_argmin", _soft_argmin, _soft_argmin_fake)
+regression_presoftmax = _register("regression_presoftmax", _presoftmax, _presoftmax_fake)
+hard_argmin = _register("hard_argmin", _hard_argmin, _argext_fake)
+hard_argmax = _register("hard_argmax", _hard_argmax, _argext_fake)

@@ -34,27 +34,31 @@ def geo(D):
 
 
 def work_lists(N, G, H, W, D, ncu):
+    """Mirror of the kernels' Sched (band_common.h): XCD-grouped segment ranges, the D passes of
+    a segment consecutive items of one workgroup."""
     T, DMAX, RW, GROUPS, npass, pw = geo(D)
     tiles = -(-W // KXT)
     nwork = tiles * H * N * G * npass
     nwg = max(8, (min(nwork, 2 * ncu) + 7) // 8 * 8)
-    q, rr = nwork >> 3, nwork & 7
+    nseg = nwork // npass
+    q, rr = nseg >> 3, nseg & 7
     for blk in range(nwg):
         grp, gi, gsz = blk & 7, blk >> 3, nwg >> 3
-        wbeg = grp * (q + 1) if grp < rr else rr * (q + 1) + (grp - rr) * q
-        wend = wbeg + q + (1 if grp < rr else 0)
-        if wbeg + gi >= wend:
+        sbeg = grp * (q + 1) if grp < rr else rr * (q + 1) + (grp - rr) * q
+        scnt = q + (1 if grp < rr else 0)
+        if gi >= scnt:
             continue
-        nitems = (wend - (wbeg + gi) + gsz - 1) // gsz
-        yield blk, [witem(wbeg, wend, gi, gsz, it) for it in range(nitems)]
+        nitems = ((scnt - gi + gsz - 1) // gsz) * npass
+        yield blk, [witem(sbeg, scnt, gi, gsz, npass, it) for it in range(nitems)]
 
 
-def witem(wbeg, wend, gi, gsz, i):
-    """Mirror of band_h2's witem(): complete aligned 8-item blocks rotated by the round i."""
-    j = gi + i * gsz
+def witem(sbeg, scnt, gi, gsz, npass, i):
+    """Mirror of Sched::item(): complete aligned 8-segment blocks rotated by the round."""
+    si, p = divmod(i, npass)
+    j = gi + si * gsz
     b = j & ~7
     rot = gsz % 8 == 0
-    return wbeg + ((b | ((j + i) & 7)) if rot and b + 8 <= wend - wbeg else j)
+    return (sbeg + ((b | ((j + si) & 7)) if rot and b + 8 <= scnt else j)) * npass + p
 
 
 def decode(w, tiles, npass, G, H, D, pw, DMAX):
