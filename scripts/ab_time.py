@@ -40,6 +40,13 @@ def ops():
                  4, 2388787200),
         "cfg4_fused_nv": (lambda: (lambda L, R: lambda: F.inner_product_soft_argmin(L, R, 256, mean=True, keep_volume=False))(
             *feats((4, 16, 1080, 1920), torch.float32)), 4, 273715200),
+        # f-4: 1x32x540x960 fp32 features warped by a 2-channel flow (sigma 4 px) / a disparity map
+        "warp2": (lambda: (lambda img, fl: lambda: F.warp_by_flow_map(img, fl))(
+            torch.randn(1, 32, 540, 960, device="cuda"), 4 * torch.randn(1, 2, 540, 960, device="cuda")),
+            1, 136857600),
+        "warp1": (lambda: (lambda img, fl: lambda: F.warp_by_flow_map(img, fl))(
+            torch.randn(1, 32, 540, 960, device="cuda"), 192 * torch.rand(1, 1, 540, 960, device="cuda")),
+            1, 134784000),
         "cfg5": (lambda: (lambda L, R: lambda: F.concat_volume(L, R, 64))(*feats((1, 128, 540, 960), torch.float16)),
                  1, 17252352000),
     }

@@ -64,7 +64,8 @@ def test_jit_trace_inner_product_network():
     net = Net().eval()
     with torch.no_grad():
         traced = torch.jit.trace(net, (l0, r0))
-    assert "stereocv::inner_product_volume" in str(traced.graph)
+    assert "stereocv::inner_product_volume" in str(traced.inlined_graph)
+    assert "stereocv::soft_argmin" in str(traced.inlined_graph)
     l1, r1 = (torch.randn(1, 32, 16, 64, device="cuda", generator=g) for _ in range(2))
     with torch.no_grad():
         torch.testing.assert_close(traced(l1, r1), net(l1, r1), rtol=0, atol=0)
