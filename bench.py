@@ -86,7 +86,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=None,
                     help="pairs per GPU per step (weak scaling; overrides --global-batch)")
     ap.add_argument("--chunk", type=int, default=None, help="pairs per kernel launch")
-    ap.add_argument("--algo", default="auto", choices=["auto", "h2", "bf16x3", "f32", "mfma", "valu"],
+    ap.add_argument("--algo", default="auto", choices=["auto", "h2", "h2db", "h2ws", "b16", "bf16x3", "f32", "mfma", "valu"],
                     help="cfg2 volume kernel of --pipeline separate")
     ap.add_argument("--pipeline", default="separate",
                     choices=["separate", "fused", "fused-novolume", "interweave"])
@@ -125,9 +125,11 @@ def kernel_name(cfg, pipeline, algo):
         return "shifted_rows_kernel" if pipeline == "interweave" else "concat_kernel"
     if cfg["op"] == "groupwise":
         return "band_h2 (NGHWD, bf16)"
-    if cfg["op"] == "inner_product" and pipeline == "separate":
+    if cfg["op"] in ("inner_product", "correlation") and pipeline == "separate":
+        # fp32 aligned rows: the double-buffered band kernel (AUTO); algos pick the others
         return {"valu": "dot_volume_valu", "f32": "ip_band_f32", "mfma": "ip_band_f32",
-                "bf16x3": "ip_band_mfma"}.get(algo, "band_h2")
+                "bf16x3": "ip_band_mfma", "h2": "band_h2", "b16": "band_b16",
+                "h2ws": "band_h2ws"}.get(algo, "band_h2db")
     return "band_h2 (fused soft-argmin)" if pipeline.startswith("fused") else "band_h2"
 
 
@@ -360,7 +362,7 @@ def cpu_baseline(cfg, a, seconds):
 
 
 # ----------------------------------------------------------------------------- PMC traffic
-EVIDENCE_ROUND = "r02"
+EVIDENCE_ROUND = "r03"
 
 
 def evidence_name(a):
@@ -376,7 +378,7 @@ def committed_traffic(a, kernel, world=1):
     rel = os.path.join("profiles", EVIDENCE_ROUND, evidence_name(a), "pmc.json")
     out = {"traffic": None, "traffic_source": None}
     # the committed passes ran this workload at N=1 with the default pairs per launch
-    if a.algo not in ("auto", "h2") or a.batch is not None or a.chunk is not None or world != 1:
+    if a.algo != "auto" or a.batch is not None or a.chunk is not None or world != 1:
         return out
     try:
         with open(os.path.join(ROOT, rel)) as f:

@@ -56,8 +56,10 @@ enum sm_ip_algo {
   /* 6: reserved (a retired warp-specialised variant, removed in round 3) */
   SM_IP_MFMA_B16 = 7,    /* the same contraction re-tiled on 16x16x32 MFMA: 16-pixel waves, four
                             waves per SIMD (fp32, 4-element aligned rows; other shapes: MFMA_H2) */
-  SM_IP_MFMA_H2DB = 8    /* MFMA_H2 with double-buffered planes: the next step is staged inside
+  SM_IP_MFMA_H2DB = 8,   /* MFMA_H2 with double-buffered planes: the next step is staged inside
                             the current step's MFMA phase (fp32, aligned rows; else MFMA_H2) */
+  SM_IP_MFMA_H2WS = 9    /* MFMA_H2DB with the volume stores moved to dedicated store waves fed
+                            through an LDS queue (fp32, aligned rows; else MFMA_H2) */
 };
 
 /* Library version (major*10000 + minor*100 + patch). */

@@ -71,10 +71,14 @@ extern "C" int sm_cv_inner_product_ex(const void* left, const void* right, void*
     case SM_IP_AUTO:  // the two-plane fp16 band kernel; odd shapes: the exact VALU kernel
     case SM_IP_MFMA_H2:
     case SM_IP_MFMA_B16:
-    case SM_IP_MFMA_H2DB: {
+    case SM_IP_MFMA_H2DB:
+    case SM_IP_MFMA_H2WS: {
       bool handled = false;
       // AUTO: fp32 aligned rows take the double-buffered band (band_h2db), the rest band_h2
-      const int variant = algo == SM_IP_MFMA_B16 ? 1 : (algo == SM_IP_MFMA_H2DB || algo == SM_IP_AUTO) ? 2 : 0;
+      const int variant = algo == SM_IP_MFMA_B16    ? 1
+                          : algo == SM_IP_MFMA_H2WS ? 3
+                          : (algo == SM_IP_MFMA_H2DB || algo == SM_IP_AUTO) ? 2
+                                                    : 0;
       int rc = band_h2_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
                              stream, &handled, variant);
       if (handled || rc != SM_OK) return rc;

@@ -24,7 +24,8 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "realtime_stereo_matcher_amd", "csrc")
-SRCS = [os.path.join(CSRC, "ip_h2.hip"), os.path.join(CSRC, "ip_b16.hip"), os.path.join(CSRC, "ip_h2db.hip")]
+SRCS = [os.path.join(CSRC, "ip_h2.hip"), os.path.join(CSRC, "ip_b16.hip"), os.path.join(CSRC, "ip_h2db.hip"),
+        os.path.join(CSRC, "ip_h2ws.hip")]
 
 
 def regs(tok):
@@ -41,7 +42,7 @@ def kernels(asm_text):
     only those loads are hand-counted (the compiler waits for its own)."""
     out, cur, in_asm = [], None, False
     for ln, line in enumerate(asm_text.splitlines(), 1):
-        if re.match(r"^_ZN4smcv6h2band(7band_h2|8band_b16|9band_h2db).*:", line):
+        if re.match(r"^_ZN4smcv6h2band(7band_h2|8band_b16|9band_h2db|9band_h2ws).*:", line):
             cur = (line.split(":")[0], [])
             out.append(cur)
             continue
@@ -141,7 +142,7 @@ def check(asm_text):
                         changed = True
         rep = []
         for i, b in enumerate(blocks):  # band_b16 must not spill at all (4 waves per SIMD)
-            transfer(b, ins_state[i], rep, no_scratch="8band_b16" in name or "9band_h2db" in name)
+            transfer(b, ins_state[i], rep, no_scratch="8band_b16" in name or "9band_h2db" in name or "9band_h2ws" in name)
         bad += [f"{name}:{r}" for r in rep]
     return bad
 
