@@ -33,6 +33,11 @@
 #ifndef SMCV_WS_ABL
 #define SMCV_WS_ABL 0
 #endif
+// 1: a store wave drains a chunk as soon as its compute wave flags it complete (LDS counters, no
+// barrier after the epilogue); 0: a barrier after the epilogue hands the whole FIFO over
+#ifndef SMCV_WS_FLAGS
+#define SMCV_WS_FLAGS 1
+#endif
 
 namespace smcv {
 namespace h2band {
@@ -56,7 +61,8 @@ struct Geo {
   static constexpr int ITEMS = 2 * GROUPS;
   static constexpr int FIFO = 2 * BUF;     // the segment's output: [wave 4][chunk NC][32][32]
   static constexpr int MAXW = FIFO + kCompute * NC * kSlot;  // 3 parity sets x (max|L|, max|R|)
-  static constexpr size_t SHM = (size_t)MAXW + 32;
+  static constexpr int FLAGS = MAXW + 32;  // per compute wave: chunks completed so far
+  static constexpr size_t SHM = (size_t)FLAGS + 16;
   static_assert(ITEMS <= kCT, "one staging item per loader lane");
   static_assert(GROUPS % 8 == 0, "8-lane write groups stay inside one chunk");
   static_assert(BUF % 1024 == 0, "plane buffers keep the swizzle's row bits");
@@ -217,7 +223,28 @@ __global__ __launch_bounds__(ws::kThreads, 3) void band_h2ws(Args args) {
   const int lane_st = rl * H * W + 4 * cl;
   const unsigned fifo = lds_addr(smem + G::FIFO);
 
-  auto epilogue_v = [&](const Work& k, auto scale, auto xlt) {
+  // Chunk hand-over (SMCV_WS_FLAGS): compute wave s counts the FIFO chunks it has completed
+  // (over all fills) in LDS word FLAGS + 4 s; store wave s waits for a chunk's count before
+  // reading it.  A wait only ever spans an interval without barriers in which the compute wave
+  // completes that chunk (its epilogue, right after the segment-end barrier), and it is bounded
+  // in any case: a wave never spins forever.
+  const unsigned flagw = lds_addr(smem + G::FLAGS);
+  auto flag_publish = [&](unsigned v) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the chunk's LDS writes are done
+    if (lane == 0)
+      *reinterpret_cast<volatile __attribute__((address_space(3))) unsigned*>(flagw + 4u * wave) = v;
+  };
+  auto flag_wait = [&](unsigned need) {
+    const unsigned fa = flagw + 4u * (unsigned)sw;
+    for (int spin = 0; spin < (1 << 16); ++spin) {
+      unsigned v;
+      asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(fa) : "memory");
+      if ((int)(__builtin_amdgcn_readfirstlane(v) - need) >= 0) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+  };
+
+  auto epilogue_v = [&](const Work& k, unsigned fbase, auto scale, auto xlt) {
     const float mul = args.mul;
     const int kk = -(kL + kR);
     const int jlane = k.js + 32 * wave + 4 * hh;
@@ -249,30 +276,31 @@ __global__ __launch_bounds__(ws::kThreads, 3) void band_h2ws(Args args) {
             }
             acc[t] = f32x16{};  // ready for the next segment's first step
             __builtin_amdgcn_sched_barrier(0);
+            if constexpr (SMCV_WS_FLAGS && a >= 0) flag_publish(fbase + (unsigned)(a + 1));
           }(),
           ...);
     }(std::make_integer_sequence<int, TMAX>{});
   };
-  auto epilogue = [&](const Work& k) {
+  auto epilogue = [&](const Work& k, unsigned fbase) {
     using TT = std::true_type;
     using FF = std::false_type;
     const bool xl = __builtin_amdgcn_readfirstlane(k.js) < 0;
     if (__builtin_amdgcn_readfirstlane(kL + kR) != 0) {
       if (xl)
-        epilogue_v(k, TT{}, TT{});
+        epilogue_v(k, fbase, TT{}, TT{});
       else
-        epilogue_v(k, TT{}, FF{});
+        epilogue_v(k, fbase, TT{}, FF{});
       return;
     }
     if (xl)
-      epilogue_v(k, FF{}, TT{});
+      epilogue_v(k, fbase, FF{}, TT{});
     else
-      epilogue_v(k, FF{}, FF{});
+      epilogue_v(k, fbase, FF{}, FF{});
   };
 
   // Store wave: chunks [c0, c1) of compute wave sw's FIFO for segment k (8 rows x 128 B per
   // store instruction, non-temporal: the volume is not re-read here)
-  auto drain = [&](const Work& k, int c0, int c1) {
+  auto drain = [&](const Work& k, int c0, int c1, unsigned fbase) {
     const bool fast = k.x0 + kXT <= W && k.Dp == DMAX;
     const int x0w = k.x0 + 32 * sw;
     unsigned rb = fifo + (unsigned)(sw * G::NC * kSlot + rl * 128 + 16 * cl);
@@ -282,6 +310,7 @@ __global__ __launch_bounds__(ws::kThreads, 3) void band_h2ws(Args args) {
     float* ob = out + (((size_t)k.n * D + k.dp) * plane_stride + (size_t)k.y * W + x0w) + ls_;
     const size_t st8 = (size_t)8 * plane_stride;
     for (int a = c0; a < c1; ++a) {
+      if constexpr (SMCV_WS_FLAGS) flag_wait(fbase + (unsigned)(a + 1));
       f32x4v v[4];
 #pragma unroll
       for (int qq = 0; qq < 4; ++qq) v[qq] = lds_load4(rb + (unsigned)(a * kSlot + 8 * qq * 128));
@@ -314,6 +343,7 @@ __global__ __launch_bounds__(ws::kThreads, 3) void band_h2ws(Args args) {
 
   // ----------------------------------------------------------------------------- main loop
   if (tid < 6) *lds_word(maxw + 4 * tid) = 0u;
+  if (tid < kCompute) *lds_word(flagw + 4 * tid) = 0u;
   __syncthreads();  // cleared before any wave publishes
   // band_h2db's loop, one copy per role (ROLE 0 compute, 1 loader, 2 store): each copy carries
   // only its role's registers (the accumulators, the staged features, the drain pointers), and
@@ -339,6 +369,7 @@ __global__ __launch_bounds__(ws::kThreads, 3) void band_h2ws(Args args) {
     Work scur = cur;                           // item sit
     bool pending = false;  // a segment's output waits in the FIFO (store: item pit)
     int pit = 0;
+    unsigned fills = 0, pfb = 0;  // FIFO fills so far; chunk-count base of the pending fill
     if constexpr (ROLE == 1) load(scur, 0);
     while (it < nitems) {
       const bool stage_ok = sit < nitems;
@@ -369,7 +400,15 @@ __global__ __launch_bounds__(ws::kThreads, 3) void band_h2ws(Args args) {
       } else {
         if (!(SMCV_WS_ABL & 1) && mul && pending) {
           // the previous segment's chunks, spread over this segment's steps
-          drain(decode(witem(pit), args, DMAX), ks * G::NC / nks, (ks + 1) * G::NC / nks);
+          // flags: half the chunks while the compute waves run the epilogue and the first step,
+          // the rest spread over the other steps; barrier hand-over: an even spread
+          auto cend = [&](int s_) {
+            if (s_ < 0) return 0;
+            if constexpr (SMCV_WS_FLAGS) return G::NC / 2 + (G::NC - G::NC / 2) * s_ / max(nks - 1, 1);
+            return (s_ + 1) * G::NC / nks;
+          };
+          const int c1 = ks == nks - 1 ? G::NC : cend(ks);
+          drain(decode(witem(pit), args, DMAX), cend(ks - 1), c1, pfb);
           if (ks == nks - 1) pending = false;
         }
       }
@@ -394,9 +433,12 @@ __global__ __launch_bounds__(ws::kThreads, 3) void band_h2ws(Args args) {
         const bool okl = ml == 0.f || (el + kL <= 15 && el + kL >= -1);
         const bool okr = mr == 0.f || (er + kR <= 15 && er + kR >= -1);
         if (fin && okl && okr) {
-          if constexpr (ROLE == 0 && !(SMCV_WS_ABL & 8)) epilogue(cur);  // the FIFO was drained
+          // (the FIFO was drained during this segment's steps)
+          if constexpr (ROLE == 0 && !(SMCV_WS_ABL & 8)) epilogue(cur, fills * (unsigned)G::NC);
           pending = true;
           pit = it;
+          pfb = fills * (unsigned)G::NC;
+          ++fills;
           redone = false;
         } else {
           const int nkl = ml > 0.f ? 13 - el : kL, nkr = mr > 0.f ? 13 - er : kR;
@@ -431,7 +473,7 @@ __global__ __launch_bounds__(ws::kThreads, 3) void band_h2ws(Args args) {
         continue;  // (it, ks) stays: its segment is multiplied again from step 0
       }
       SM_STAMP(3);
-      if (mul && ks == nks - 1) __syncthreads();  // the FIFO is complete for the store waves
+      if (!SMCV_WS_FLAGS && mul && ks == nks - 1) __syncthreads();  // the FIFO is complete
       SM_STAMP(4);
       // advance: the staged step is multiplied next, the step after it is staged
       cur = scur;
@@ -451,7 +493,7 @@ __global__ __launch_bounds__(ws::kThreads, 3) void band_h2ws(Args args) {
       }
     }
     if constexpr (ROLE == 2 && !(SMCV_WS_ABL & 1)) {
-      if (pending) drain(decode(witem(pit), args, DMAX), 0, G::NC);  // the last segment
+      if (pending) drain(decode(witem(pit), args, DMAX), 0, G::NC, pfb);  // the last segment
     }
     SM_STAMP_FLUSH
   };
