@@ -185,6 +185,18 @@ int sm_warp_by_flow(const void* image, const void* flow, void* out, int dtype,
                     int64_t N, int64_t C, int64_t Hi, int64_t Wi, int64_t H, int64_t W,
                     int64_t flow_channels, const int64_t* image_strides,
                     const int64_t* flow_strides, void* stream);
+/* The same warp with a caller-provided device workspace (16-B aligned): two-channel flows over
+ * at most 64 channels then sample a channel-last copy of the image (one 128-B line per corner
+ * and pixel at C = 32 instead of one per corner, pixel and channel).  Same results.
+ * sm_warp_by_flow_workspace_bytes gives the size (0: the shape does not use one; any workspace,
+ * or none, is then accepted and ignored). */
+int64_t sm_warp_by_flow_workspace_bytes(int64_t N, int64_t C, int64_t Hi, int64_t Wi,
+                                        int64_t flow_channels);
+int sm_warp_by_flow_ws(const void* image, const void* flow, void* out, int dtype,
+                       int64_t N, int64_t C, int64_t Hi, int64_t Wi, int64_t H, int64_t W,
+                       int64_t flow_channels, const int64_t* image_strides,
+                       const int64_t* flow_strides, void* workspace, int64_t workspace_bytes,
+                       void* stream);
 
 /* §8f-2: MobileStereoNetV4's cost volume -- model/mobile_stereo_net_v4.py:443-461 with the
  * stacks :317-335 (replaces the 48-iteration interweave -> conv3d -> volume11 loop).

@@ -39,10 +39,13 @@ SIGNATURES = {
     "sm_regress_softargmin": [_p, _p, _i, _l, _l, _l, _l, _i, _lp, _p],
     "sm_regress_argext": [_p, _p, _i, _l, _l, _l, _l, _i, _lp, _p],
     "sm_warp_by_flow": [_p, _p, _p, _i, _l, _l, _l, _l, _l, _l, _l, _lp, _lp, _p],
+    "sm_warp_by_flow_workspace_bytes": [_l, _l, _l, _l, _l],
+    "sm_warp_by_flow_ws": [_p, _p, _p, _i, _l, _l, _l, _l, _l, _l, _l, _lp, _lp, _p, _l, _p],
     "sm_v4_volume_workspace_bytes": [_l, _l, _l],
     "sm_v4_volume": [_p, _p, _p, _i, _l, _l, _l, _l, _l, _lp, _lp] + [_p] * 9 + [_l, _p],
 }
 _RESTYPE = {"sm_last_error": ctypes.c_char_p, "sm_v4_volume_workspace_bytes": ctypes.c_int64,
+            "sm_warp_by_flow_workspace_bytes": ctypes.c_int64,
             "sm_cv_inner_product_softargmin_workspace_bytes": ctypes.c_int64}
 
 _lock = threading.Lock()

@@ -46,7 +46,9 @@ int argext_entry(const void* volume, int64_t* out, int dtype, int64_t N, int64_t
                  int64_t W, int mode, const int64_t* vol_strides, void* stream);
 int warp_entry(const void* image, const void* flow, void* out, int dtype, int64_t N, int64_t C,
                int64_t Hi, int64_t Wi, int64_t H, int64_t W, int64_t flow_channels,
-               const int64_t* image_strides, const int64_t* flow_strides, void* stream);
+               const int64_t* image_strides, const int64_t* flow_strides, void* stream,
+               void* workspace, int64_t workspace_bytes);
+int64_t warp_workspace_bytes(int64_t N, int64_t C, int64_t Hi, int64_t Wi, int64_t flow_channels);
 }  // namespace smcv
 
 using namespace smcv;
@@ -243,7 +245,23 @@ extern "C" int sm_warp_by_flow(const void* image, const void* flow, void* out, i
                                const int64_t* flow_strides, void* stream) {
   SM_ENTRY_BEGIN
   return warp_entry(image, flow, out, dtype, N, C, Hi, Wi, H, W, flow_channels, image_strides,
-                    flow_strides, stream);
+                    flow_strides, stream, nullptr, 0);
+}
+
+extern "C" int64_t sm_warp_by_flow_workspace_bytes(int64_t N, int64_t C, int64_t Hi, int64_t Wi,
+                                                   int64_t flow_channels) {
+  return warp_workspace_bytes(N, C, Hi, Wi, flow_channels);
+}
+
+extern "C" int sm_warp_by_flow_ws(const void* image, const void* flow, void* out, int dtype,
+                                  int64_t N, int64_t C, int64_t Hi, int64_t Wi, int64_t H, int64_t W,
+                                  int64_t flow_channels, const int64_t* image_strides,
+                                  const int64_t* flow_strides, void* workspace,
+                                  int64_t workspace_bytes, void* stream) {
+  SM_ENTRY_BEGIN
+  if (workspace_bytes < 0) return fail(SM_EINVAL, "warp_by_flow_map: negative workspace size");
+  return warp_entry(image, flow, out, dtype, N, C, Hi, Wi, H, W, flow_channels, image_strides,
+                    flow_strides, stream, workspace, workspace_bytes);
 }
 
 extern "C" int64_t sm_v4_volume_workspace_bytes(int64_t N, int64_t H, int64_t W) {

@@ -39,16 +39,15 @@ struct WarpArgs {
   float dw, dh;           // (float)(w - 1.0), (float)(h - 1.0)
 };
 
-__global__ __launch_bounds__(kWarpThreads) void warp_kernel(WarpArgs a, int cpb) {
+// Output pixel (n, y, x): the four bilinear weights (nw, ne, sw, se), the top-left corner
+// (x0, y0) and which corners lie inside the image.  The reference's fp32 operation sequence.
+struct Corners {
+  float w[4];
+  bool ok[4];
+  int x0, y0;
+};
+__device__ __forceinline__ Corners corners_of(const WarpArgs& a, int n, int y, int x) {
 #pragma clang fp contract(off)  // separate roundings, as the reference's grid math and blend
-  // block (pixel chunk, channel chunk, n): the waves in flight share a few channel planes
-  const int n = blockIdx.z;
-  const int cbeg = blockIdx.y * cpb, cend = min(a.C, cbeg + cpb);
-  const int64_t p = (int64_t)blockIdx.x * kWarpThreads + threadIdx.x;
-  const int64_t HW = (int64_t)a.H * a.W;
-  if (p >= HW) return;
-  const int y = (int)(p / a.W);
-  const int x = (int)(p - (int64_t)y * a.W);
   const float* fl = a.flow + n * a.fsn + (int64_t)y * a.fsh + x;
   // grid, exactly as the reference: (x - f) -> 2 * . / (w - 1) - 1   (tools/warp.py:19-36)
   float gx = (float)x - fl[0];
@@ -62,17 +61,39 @@ __global__ __launch_bounds__(kWarpThreads) void warp_kernel(WarpArgs a, int cpb)
   const float fx0 = floorf(ix), fy0 = floorf(iy);
   const float dx = ix - fx0, dy = iy - fy0;
   const float ex = 1.0f - dx, sy = 1.0f - dy;
-  float w[4] = {sy * ex, sy * dx, dy * ex, dy * dx};  // nw, ne, sw, se
-  int64_t off[4];
-  bool ok[4];
+  Corners q;
+  q.w[0] = sy * ex;  // nw
+  q.w[1] = sy * dx;  // ne
+  q.w[2] = dy * ex;  // sw
+  q.w[3] = dy * dx;  // se
   const bool finite = fabsf(ix) < 2.0e9f && fabsf(iy) < 2.0e9f;  // int conversion in range
-  const int x0 = finite ? (int)fx0 : -2, y0 = finite ? (int)fy0 : -2;
+  q.x0 = finite ? (int)fx0 : -2;
+  q.y0 = finite ? (int)fy0 : -2;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const int xx = x0 + (k & 1), yy = y0 + (k >> 1);
-    ok[k] = finite && xx >= 0 && xx < a.Wi && yy >= 0 && yy < a.Hi;
-    off[k] = ok[k] ? (int64_t)yy * a.ish + xx : 0;
+    const int xx = q.x0 + (k & 1), yy = q.y0 + (k >> 1);
+    q.ok[k] = finite && xx >= 0 && xx < a.Wi && yy >= 0 && yy < a.Hi;
   }
+  return q;
+}
+
+__global__ __launch_bounds__(kWarpThreads) void warp_kernel(WarpArgs a, int cpb) {
+#pragma clang fp contract(off)  // separate roundings, as the reference's blend
+  // block (pixel chunk, channel chunk, n): the waves in flight share a few channel planes
+  const int n = blockIdx.z;
+  const int cbeg = blockIdx.y * cpb, cend = min(a.C, cbeg + cpb);
+  const int64_t p = (int64_t)blockIdx.x * kWarpThreads + threadIdx.x;
+  const int64_t HW = (int64_t)a.H * a.W;
+  if (p >= HW) return;
+  const int y = (int)(p / a.W);
+  const int x = (int)(p - (int64_t)y * a.W);
+  const Corners q = corners_of(a, n, y, x);
+  const float* w = q.w;
+  const bool* ok = q.ok;
+  const int x0 = q.x0, y0 = q.y0;
+  int64_t off[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) off[k] = ok[k] ? (int64_t)(y0 + (k >> 1)) * a.ish + x0 + (k & 1) : 0;
   const float* ib = a.img + n * a.isn;
   float* ob = a.out + ((int64_t)n * a.C) * HW + p;
   int c = cbeg;
@@ -119,6 +140,97 @@ __global__ __launch_bounds__(kWarpThreads) void warp_kernel(WarpArgs a, int cpb)
 #pragma unroll
     for (int k = 0; k < 4; ++k) v[k] = ok[k] ? ib[(int64_t)c * a.isc + off[k]] : 0.f;
     ob[(int64_t)c * HW] = v[0] * w[0] + v[1] * w[1] + v[2] * w[2] + v[3] * w[3];
+  }
+}
+
+// Two-channel flows, channel-last: a flow scatters the rows a wave samples, so in the (N, C, H, W)
+// image every corner of every channel is its own 128-B line (warp_kernel: 0.18 of HBM at a
+// sigma-4 flow).  warp_to_nhwc first copies the image to (N, Hi, Wi, Cp) (Cp = C rounded up to 4,
+// zero padded; coalesced reads per channel row, contiguous 16-B writes per pixel), then
+// warp_gather_nhwc gives a pixel's 4-channel groups to consecutive lanes: one corner of a pixel
+// is Cp * 4 contiguous bytes (one line at C = 32), the blend is warp_kernel's, and the block's
+// 64 x C outputs leave through LDS as coalesced channel rows.
+constexpr int kNhwcPx = 64;     // pixels per transpose block
+constexpr int kGatherPx = 128;  // pixels per gather block (<= kWarpThreads: one corner lane each)
+
+__global__ __launch_bounds__(kWarpThreads) void warp_to_nhwc(WarpArgs a, float* ws, int Cp) {
+  extern __shared__ float tile[];  // [64 px][Cp + 1]
+  const int n = blockIdx.z, yy = blockIdx.y, x0 = blockIdx.x * kNhwcPx;
+  const int np = min(kNhwcPx, a.Wi - x0);
+  const int S = Cp + 1;
+  const float* src = a.img + n * a.isn + (int64_t)yy * a.ish + x0;
+  for (int i = threadIdx.x; i < Cp * kNhwcPx; i += kWarpThreads) {
+    const int c = i / kNhwcPx, px = i % kNhwcPx;
+    tile[px * S + c] = (c < a.C && px < np) ? src[(int64_t)c * a.isc + px] : 0.f;
+  }
+  __syncthreads();
+  const int G = Cp >> 2;
+  float4* dst = reinterpret_cast<float4*>(ws + (((int64_t)n * a.Hi + yy) * a.Wi + x0) * Cp);
+  for (int i = threadIdx.x; i < np * G; i += kWarpThreads) {
+    const int px = i / G, g = i - px * G;
+    const float* s = tile + px * S + 4 * g;
+    dst[i] = make_float4(s[0], s[1], s[2], s[3]);
+  }
+}
+
+__global__ __launch_bounds__(kWarpThreads) void warp_gather_nhwc(WarpArgs a, const float* ws, int Cp) {
+#pragma clang fp contract(off)  // separate roundings, as the reference's blend
+  // LDS: the block's 128 pixels' corners (4 image-pixel indices, -1 outside; 4 weights), then
+  // the outputs [C][128 + 1]
+  __shared__ int cidx[kGatherPx][4];
+  __shared__ float cw[kGatherPx][4];
+  extern __shared__ float otile[];
+  const int n = blockIdx.y;
+  const int64_t HW = (int64_t)a.H * a.W;
+  const int64_t p0 = (int64_t)blockIdx.x * kGatherPx;
+  const int np = (int)min<int64_t>(kGatherPx, HW - p0);
+  if (threadIdx.x < np) {  // corners once per pixel (flow reads coalesced)
+    const int64_t p = p0 + threadIdx.x;
+    const int y = (int)(p / a.W), x = (int)(p - (int64_t)y * a.W);
+    const Corners q = corners_of(a, n, y, x);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      cidx[threadIdx.x][k] = q.ok[k] ? (q.y0 + (k >> 1)) * a.Wi + q.x0 + (k & 1) : -1;
+      cw[threadIdx.x][k] = q.w[k];
+    }
+  }
+  __syncthreads();
+  const int G = Cp >> 2;
+  const float4* img = reinterpret_cast<const float4*>(ws + (int64_t)n * a.Hi * a.Wi * Cp);
+  constexpr int U = 4;  // items per lane in flight: 16 gathers issued before the first blend
+  for (int i0 = threadIdx.x; i0 < np * G; i0 += U * kWarpThreads) {
+    float4 v[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * kWarpThreads;
+      const int px = min(i / G, np - 1), g = i - (i / G) * G;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int ci = i < np * G ? cidx[px][k] : -1;
+        v[u][k] = ci >= 0 ? img[(int64_t)ci * G + g] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * kWarpThreads;
+      if (i >= np * G) break;
+      const int px = i / G, g = i - px * G;
+      const float* w = cw[px];
+      const float4* vv = v[u];
+      const float r[4] = {vv[0].x * w[0] + vv[1].x * w[1] + vv[2].x * w[2] + vv[3].x * w[3],
+                          vv[0].y * w[0] + vv[1].y * w[1] + vv[2].y * w[2] + vv[3].y * w[3],
+                          vv[0].z * w[0] + vv[1].z * w[1] + vv[2].z * w[2] + vv[3].z * w[3],
+                          vv[0].w * w[0] + vv[1].w * w[1] + vv[2].w * w[2] + vv[3].w * w[3]};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (4 * g + j < a.C) otile[(4 * g + j) * (kGatherPx + 1) + px] = r[j];
+    }
+  }
+  __syncthreads();
+  float* ob = a.out + (int64_t)n * a.C * HW + p0;
+  for (int i = threadIdx.x; i < a.C * kGatherPx; i += kWarpThreads) {
+    const int c = i / kGatherPx, px = i % kGatherPx;
+    if (px < np) ob[(int64_t)c * HW + px] = otile[c * (kGatherPx + 1) + px];
   }
 }
 
@@ -228,9 +340,19 @@ __global__ __launch_bounds__(kWarpThreads) void warp_rows_kernel(WarpArgs a, int
 
 }  // namespace
 
+// Bytes of the channel-last image copy the two-channel path uses (0: the shape takes the other
+// kernels).
+int64_t warp_workspace_bytes(int64_t N, int64_t C, int64_t Hi, int64_t Wi, int64_t flow_channels) {
+  if (flow_channels != 2 || N <= 0 || C <= 0 || C > 64 || Hi <= 0 || Wi <= 0) return 0;
+  const int64_t Cp = (C + 3) / 4 * 4;
+  if (Hi * Wi >= ((int64_t)1 << 31) || N * Hi * Wi * Cp >= ((int64_t)1 << 40)) return 0;
+  return N * Hi * Wi * Cp * 4;
+}
+
 int warp_entry(const void* image, const void* flow, void* out, int dtype, int64_t N, int64_t C,
                int64_t Hi, int64_t Wi, int64_t H, int64_t W, int64_t flow_channels,
-               const int64_t* image_strides, const int64_t* flow_strides, void* stream) {
+               const int64_t* image_strides, const int64_t* flow_strides, void* stream,
+               void* workspace, int64_t workspace_bytes) {
   if (dtype != SM_F32) return fail(SM_EDTYPE, "warp_by_flow_map: float32 image and flow only");
   if (N < 0 || C < 0 || Hi < 0 || Wi < 0 || H < 0 || W < 0) return fail(SM_EINVAL, "negative size");
   if (flow_channels != 1 && flow_channels != 2)
@@ -278,6 +400,19 @@ int warp_entry(const void* image, const void* flow, void* out, int dtype, int64_
     else
       hipLaunchKernelGGL(warp_rows_kernel<false>, grid, dim3(kWarpThreads), shm, st, a, CC);
     return check_launch("warp_rows_kernel");
+  }
+  const int64_t need = warp_workspace_bytes(N, C, Hi, Wi, flow_channels);
+  if (need > 0 && workspace != nullptr && workspace_bytes >= need &&
+      (reinterpret_cast<uintptr_t>(workspace) & 15u) == 0 && Hi <= 65535) {
+    const int Cp = (int)((C + 3) / 4 * 4);
+    float* ws = static_cast<float*>(workspace);
+    hipLaunchKernelGGL(warp_to_nhwc, dim3((unsigned)ceil_div(Wi, kNhwcPx), (unsigned)Hi, (unsigned)N),
+                       dim3(kWarpThreads), (size_t)kNhwcPx * (Cp + 1) * 4, st, a, ws, Cp);
+    if (int rc = check_launch("warp_to_nhwc")) return rc;
+    hipLaunchKernelGGL(warp_gather_nhwc, dim3((unsigned)ceil_div(H * W, kGatherPx), (unsigned)N),
+                       dim3(kWarpThreads), (size_t)C * (kGatherPx + 1) * 4, st, a,
+                       static_cast<const float*>(ws), Cp);
+    return check_launch("warp_gather_nhwc");
   }
   // channels per block: the waves in flight share a few channel planes (1x32x540x960, sigma-4
   // flow: 94-96 us with 8 channels per block against 100 us with all 32; r03 A/B).  An LDS

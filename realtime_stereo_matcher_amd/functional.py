@@ -511,7 +511,11 @@ def warp_by_flow_map(image, flow):
     out = torch.empty((N, C, h, w), dtype=torch.float32, device=dev)
     if out.numel():
         lib = _lib.load()
-        _lib.check(lib.sm_warp_by_flow(_ptr(image), _ptr(flow), _ptr(out), _lib.SM_F32, N, C, Hi,
-                                       Wi, h, w, c, _lib.strides_arg(image),
-                                       _lib.strides_arg(flow), _stream(dev)), "sm_warp_by_flow")
+        # two-channel flows sample a channel-last copy of the image (csrc/warp.hip)
+        nws = int(lib.sm_warp_by_flow_workspace_bytes(N, C, Hi, Wi, c))
+        ws = torch.empty(nws, dtype=torch.uint8, device=dev) if nws > 0 else None
+        _lib.check(lib.sm_warp_by_flow_ws(_ptr(image), _ptr(flow), _ptr(out), _lib.SM_F32, N, C, Hi,
+                                          Wi, h, w, c, _lib.strides_arg(image),
+                                          _lib.strides_arg(flow), _ptr(ws) if ws is not None else None,
+                                          nws, _stream(dev)), "sm_warp_by_flow_ws")
     return out if odt == torch.float32 else out.to(odt)

@@ -19,6 +19,18 @@ def feats(shape, dtype):
             torch.randn(*shape, device="cuda", generator=g).to(dtype))
 
 
+def _warp_nows(img, flow):
+    """The warp without a workspace (sm_warp_by_flow: warp_kernel for two-channel flows)."""
+    from realtime_stereo_matcher_amd import _lib
+    N, C, Hi, Wi = img.shape
+    _, c, h, w = flow.shape
+    out = torch.empty((N, C, h, w), dtype=torch.float32, device="cuda")
+    _lib.check(_lib.load().sm_warp_by_flow(img.data_ptr(), flow.data_ptr(), out.data_ptr(), _lib.SM_F32,
+                                           N, C, Hi, Wi, h, w, c, None, None,
+                                           torch.cuda.current_stream().cuda_stream), "warp")
+    return out
+
+
 def ops():
     return {
         # name: (setup -> callable, pairs per launch, algorithmic bytes per pair)
@@ -44,6 +56,9 @@ def ops():
             *feats((4, 16, 1080, 1920), torch.float32)), 4, 273715200),
         # f-4: 1x32x540x960 fp32 features warped by a 2-channel flow (sigma 4 px) / a disparity map
         "warp2": (lambda: (lambda img, fl: lambda: F.warp_by_flow_map(img, fl))(
+            torch.randn(1, 32, 540, 960, device="cuda"), 4 * torch.randn(1, 2, 540, 960, device="cuda")),
+            1, 136857600),
+        "warp2_nows": (lambda: (lambda img, fl: lambda: _warp_nows(img, fl))(
             torch.randn(1, 32, 540, 960, device="cuda"), 4 * torch.randn(1, 2, 540, 960, device="cuda")),
             1, 136857600),
         "warp1": (lambda: (lambda img, fl: lambda: F.warp_by_flow_map(img, fl))(

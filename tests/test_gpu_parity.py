@@ -812,3 +812,56 @@ def test_warp_full_size_rows():
     rows = [0, 1, 269, 538, 539]
     ref = O.warp_by_flow_map(host(I), host(Fl), rows=rows)
     np.testing.assert_allclose(host(out[:, :, rows]), ref, atol=TOL, rtol=0)
+
+
+def _warp_no_workspace(img, flow):
+    """The warp through sm_warp_by_flow (no workspace: warp_kernel / warp_rows_kernel)."""
+    from realtime_stereo_matcher_amd import _lib
+
+    N, C, Hi, Wi = img.shape
+    _, c, h, w = flow.shape
+    out = torch.empty((N, C, h, w), dtype=torch.float32, device="cuda")
+    _lib.check(_lib.load().sm_warp_by_flow(img.data_ptr(), flow.data_ptr(), out.data_ptr(), _lib.SM_F32,
+                                           N, C, Hi, Wi, h, w, c, _lib.strides_arg(img),
+                                           _lib.strides_arg(flow), torch.cuda.current_stream().cuda_stream),
+               "sm_warp_by_flow")
+    return out
+
+
+@pytest.mark.parametrize("C", [1, 3, 4, 5, 32, 64, 65])
+def test_warp_channel_last_path_bit_identical(C):
+    """Two-channel flows take the channel-last gather (warp_to_nhwc + warp_gather_nhwc, C <= 64)
+    when functional passes its workspace: bit-identical to warp_kernel, padding, NaN flows,
+    a channel-strided image and a resized output grid included; and within TOL of the oracle."""
+    from realtime_stereo_matcher_amd import _lib
+    from realtime_stereo_matcher_amd.functional import warp_by_flow_map
+
+    g = torch.Generator(device="cuda").manual_seed(100 + C)
+    img = torch.randn(2, 2 * C, 19, 70, device="cuda", generator=g)[:, ::2]  # channel-strided
+    flow = torch.randn(2, 2, 23, 67, device="cuda", generator=g) * 6
+    flow[0, 0, 0, :5] = float("nan")
+    flow[1, 1, 3, :4] = 1e9
+    flow[1, :, -1, -3:] = 2.0
+    got = warp_by_flow_map(img, flow)
+    assert (int(_lib.load().sm_warp_by_flow_workspace_bytes(2, C, 19, 70, 2)) > 0) == (C <= 64)
+    want = _warp_no_workspace(img, flow)
+    assert torch.equal(torch.nan_to_num(got, nan=7.0), torch.nan_to_num(want, nan=7.0))
+    assert torch.equal(torch.isnan(got), torch.isnan(want))
+    if C in (3, 32):
+        ref = O.warp_by_flow_map(host(img), host(flow))
+        np.testing.assert_allclose(host(got), ref, atol=TOL, rtol=0)
+
+
+def test_warp_full_size_two_channel_flow():
+    """1x32x540x960 features, a sigma-4 two-channel flow (the bench's warp2 shape) through the
+    channel-last path: sampled rows against the oracle and the whole plane against warp_kernel."""
+    from realtime_stereo_matcher_amd.functional import warp_by_flow_map
+
+    g = torch.Generator(device="cuda").manual_seed(6)
+    I = torch.randn(1, 32, 540, 960, device="cuda", generator=g)
+    Fl = torch.randn(1, 2, 540, 960, device="cuda", generator=g) * 4
+    out = warp_by_flow_map(I, Fl)
+    assert torch.equal(out, _warp_no_workspace(I, Fl))
+    rows = [0, 1, 270, 539]
+    ref = O.warp_by_flow_map(host(I), host(Fl), rows=rows)
+    np.testing.assert_allclose(host(out[:, :, rows]), ref, atol=TOL, rtol=0)
