@@ -250,5 +250,102 @@ struct Sched {
   }
 };
 
+// Soft-argmin straight from a wave's band accumulators (the fused pass, f-1).  Lane (lr, hh)
+// holds, for pixel x0 + 32 wave + lr, the cells of local disparity dl = 32 (T-1-t) + u - c_i
+// (block t, element i, u = lr - 4 hh), and the lane pair (lr, 0), (lr, 1) holds every d of the
+// pixel exactly once.  One pass, block by block (every accumulator element read once): the
+// block's maximum, the running sums rescaled when it grows, the block's exps summed in fp32 and
+// carried into fp64.  Cells outside 0 <= dl < Dp enter as -inf (e = 0); only the first and the
+// last block can hold such cells when Dp == DMAX.  No NaN / inf flags: a NaN cell makes its e
+// NaN, a +inf maximum makes (inf - inf) NaN, an all -inf pixel gives 0 / 0 -- torch's NaN each
+// time.  The shift max(m, -FLT_MAX) keeps exp2 finite-argument when no cell is finite yet.  The
+// pair merges by one shuffle; lane hh = 0 stores the disparity (one pass) or the pass's partial
+// state (several D passes, args.ws_m).  SCALE multiplies back by 2^-(kL+kR); XLT forces the
+// cells x < d (R pad rows) to 0, as the volume has them.  WS: the partial-state form exists
+// (several D passes); without it only the disparity store is compiled.
+template <int TMAX, bool MEAN, bool SCALE, bool XLT, bool WS = true>
+__device__ __forceinline__ void fused_softargmin(const f32x16 (&acc)[TMAX], const Args& args,
+                                                 const Work& k, int kL, int kR, int wave, int lr,
+                                                 int hh) {
+  constexpr int DMAX = 32 * (TMAX - 1);
+  const float mul = args.mul;
+  const int kk = -(kL + kR);
+  const int jlane = k.js + 32 * wave + 4 * hh;
+  const int u0 = lr - 4 * hh;
+  auto value = [&](int t, int i) {
+    const int ci = (i & 3) + 8 * (i >> 2);
+    float val = acc[t][i];
+    if (MEAN) val *= mul;
+    if constexpr (SCALE) val = __builtin_ldexpf(val, kk);
+    if constexpr (XLT) val = jlane + 32 * t + ci >= 0 ? val : 0.f;
+    return val;
+  };
+  constexpr float kL2E = 1.4426950408889634f;
+  const bool full = k.Dp == DMAX;
+  float m = -INFINITY;
+  double s = 0.0, tt = 0.0;
+  auto block = [&](auto tc, auto maskc) {
+    constexpr int t = decltype(tc)::value;
+    int ub = u0 + 32 * (TMAX - 1 - t);  // dl = ub - c_i; opaque per block (not hoisted)
+    asm volatile("" : "+v"(ub));
+    float v[16];
+    float bm = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int ci = (i & 3) + 8 * (i >> 2);
+      float x = value(t, i);
+      if constexpr (decltype(maskc)::value) x = (unsigned)(ub - ci) < (unsigned)k.Dp ? x : -INFINITY;
+      v[i] = x;
+      bm = fmaxf(bm, x);
+    }
+    const float nm = fmaxf(m, bm);
+    const float sh = fmaxf(nm, -3.402823466e38f);
+    const float f = __builtin_amdgcn_exp2f((m - sh) * kL2E);
+    float ps = 0.f, pc = 0.f;  // sum e, sum c_i e
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float e = __builtin_amdgcn_exp2f((v[i] - sh) * kL2E);
+      ps += e;
+      pc = fmaf((float)((i & 3) + 8 * (i >> 2)), e, pc);
+    }
+    s = s * (double)f + (double)ps;
+    tt = tt * (double)f + (double)ub * (double)ps - (double)pc;  // sum (ub - c_i) e
+    m = nm;
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // the first and the last block always straddle the band's ends; the middle ones only when
+  // Dp < DMAX (a uniform branch: the common full-D item runs them unmasked)
+  using TT = std::true_type;
+  using FF = std::false_type;
+  [&]<int... T_>(std::integer_sequence<int, T_...>) {
+    ((T_ == 0 || T_ == TMAX - 1
+          ? block(std::integral_constant<int, T_>{}, TT{})
+          : (full ? block(std::integral_constant<int, T_>{}, FF{})
+                  : block(std::integral_constant<int, T_>{}, TT{}))),
+     ...);
+  }(std::make_integer_sequence<int, TMAX>{});
+  // the other row half of the pixel
+  const float M = fmaxf(m, __shfl_xor(m, 32));
+  const double g = (double)__builtin_amdgcn_exp2f((m - fmaxf(M, -3.402823466e38f)) * kL2E);
+  s *= g;
+  tt *= g;
+  s += __shfl_xor(s, 32);
+  tt += __shfl_xor(tt, 32);
+  const int x = k.x0 + 32 * wave + lr;
+  if (hh == 0 && x < args.W) {
+    const size_t px = ((size_t)k.n * args.H + k.y) * args.W + x;
+    if (WS && args.ws_m != nullptr) {  // one of several D passes: its partial state, d global
+      typedef __attribute__((address_space(1))) void gvoid;
+      const size_t o = (size_t)k.pass * ((size_t)args.nhw) + px;
+      *reinterpret_cast<__attribute__((address_space(1))) double*>((gvoid*)(args.ws_s + o)) = s;
+      *reinterpret_cast<__attribute__((address_space(1))) double*>((gvoid*)(args.ws_t + o)) =
+          tt + (double)k.dp * s;
+      store_one<float>(args.ws_m + o, M);
+    } else {
+      store_one<float>(args.disp + px, (float)(tt / s));
+    }
+  }
+}
+
 }  // namespace h2band
 }  // namespace smcv

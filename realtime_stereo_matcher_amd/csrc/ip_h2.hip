@@ -333,95 +333,12 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
   const unsigned rdbase = LAYOUT == kNDHW ? ringw + (unsigned)(rl * 128 + 16 * cl)
                                           : ringw + (unsigned)(rl * 384 + 16 * cl);
 
-  // Fused soft-argmin straight from the accumulators: lane (lr, hh) holds, for pixel x0w + lr,
-  // the cells of local disparity dl = 32 (T-1-t) + u - c_i (block t, element i), and the lane
-  // pair (lr, 0), (lr, 1) holds every d of the pixel exactly once.  Pass 1: the pixel's maximum
-  // (and NaN); pass 2: sums of e = exp(v - M) and dl e, fp32 within a block, fp64 across blocks;
-  // the pair merges by one shuffle.  No ring, no LDS: the volume-free kernel never shears.
+  // Fused soft-argmin straight from the accumulators (fused_softargmin, band_common.h; shared
+  // with band_h2db's FUSE 1).  No ring, no LDS: the volume-free kernel never shears.
   auto fuse_regs = [&](const Work& k, auto scale, auto xlt) {
-    const float mul = args.mul;
-    const int kk = -(kL + kR);
-    const int jlane = k.js + 32 * wave + 4 * hh;
-    const int u0 = lr - 4 * hh;
-    auto value = [&](int t, int i) {
-      const int ci = (i & 3) + 8 * (i >> 2);
-      float val = acc[t][i];
-      if (MEAN) val *= mul;
-      if constexpr (decltype(scale)::value) val = __builtin_ldexpf(val, kk);
-      if constexpr (decltype(xlt)::value) val = jlane + 32 * t + ci >= 0 ? val : 0.f;
-      return val;
-    };
-    // One pass, block by block (every accumulator element read once): the block's maximum, the
-    // running sums rescaled when it grows, the block's exps summed in fp32 and carried into
-    // fp64.  Cells outside 0 <= dl < Dp enter as -inf (e = 0); only the first and the last block
-    // can hold such cells when Dp == DMAX.  No NaN / inf flags: a NaN cell makes its e NaN, a
-    // +inf maximum makes (inf - inf) NaN, an all -inf pixel gives 0 / 0 -- torch's NaN each time.
-    // The shift max(m, -FLT_MAX) keeps exp2 finite-argument when no cell is finite yet.
-    constexpr float kL2E = 1.4426950408889634f;
-    const bool full = k.Dp == DMAX;
-    float m = -INFINITY;
-    double s = 0.0, tt = 0.0;
-    auto block = [&](auto tc, auto maskc) {
-      constexpr int t = decltype(tc)::value;
-      int ub = u0 + 32 * (TMAX - 1 - t);  // dl = ub - c_i; opaque per block (not hoisted)
-      asm volatile("" : "+v"(ub));
-      float v[16];
-      float bm = -INFINITY;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int ci = (i & 3) + 8 * (i >> 2);
-        float x = value(t, i);
-        if constexpr (decltype(maskc)::value) x = (unsigned)(ub - ci) < (unsigned)k.Dp ? x : -INFINITY;
-        v[i] = x;
-        bm = fmaxf(bm, x);
-      }
-      const float nm = fmaxf(m, bm);
-      const float sh = fmaxf(nm, -3.402823466e38f);
-      const float f = __builtin_amdgcn_exp2f((m - sh) * kL2E);
-      float ps = 0.f, pc = 0.f;  // sum e, sum c_i e
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float e = __builtin_amdgcn_exp2f((v[i] - sh) * kL2E);
-        ps += e;
-        pc = fmaf((float)((i & 3) + 8 * (i >> 2)), e, pc);
-      }
-      s = s * (double)f + (double)ps;
-      tt = tt * (double)f + (double)ub * (double)ps - (double)pc;  // sum (ub - c_i) e
-      m = nm;
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    // the first and the last block always straddle the band's ends; the middle ones only when
-    // Dp < DMAX (a uniform branch: the common full-D item runs them unmasked)
-    using TT = std::true_type;
-    using FF = std::false_type;
-    [&]<int... T_>(std::integer_sequence<int, T_...>) {
-      ((T_ == 0 || T_ == TMAX - 1
-            ? block(std::integral_constant<int, T_>{}, TT{})
-            : (full ? block(std::integral_constant<int, T_>{}, FF{})
-                    : block(std::integral_constant<int, T_>{}, TT{}))),
-       ...);
-    }(std::make_integer_sequence<int, TMAX>{});
-    // the other row half of the pixel
-    const float M = fmaxf(m, __shfl_xor(m, 32));
-    const double g = (double)__builtin_amdgcn_exp2f((m - fmaxf(M, -3.402823466e38f)) * kL2E);
-    s *= g;
-    tt *= g;
-    s += __shfl_xor(s, 32);
-    tt += __shfl_xor(tt, 32);
-    const int x = k.x0 + 32 * wave + lr;
-    if (hh == 0 && x < W) {
-      const size_t px = ((size_t)k.n * H + k.y) * W + x;
-      if (args.ws_m != nullptr) {  // one of several D passes: its partial state, d global
-        typedef __attribute__((address_space(1))) void gvoid;
-        const size_t o = (size_t)k.pass * ((size_t)args.nhw) + px;
-        *reinterpret_cast<__attribute__((address_space(1))) double*>((gvoid*)(args.ws_s + o)) = s;
-        *reinterpret_cast<__attribute__((address_space(1))) double*>((gvoid*)(args.ws_t + o)) =
-            tt + (double)k.dp * s;
-        store_one<float>(args.ws_m + o, M);
-      } else {
-        store_one<float>(args.disp + px, (float)(tt / s));
-      }
-    }
+    if constexpr (std::is_same<T, float>::value)
+      fused_softargmin<TMAX, MEAN, decltype(scale)::value, decltype(xlt)::value>(acc, args, k, kL, kR,
+                                                                                 wave, lr, hh);
   };
 
   // SCALE: multiply back by 2^-(kL+kR); XLT: the segment has cells x < d (R pad rows), forced
@@ -887,6 +804,8 @@ namespace h2band {
 int band_b16_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled);
 int band_h2db_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled);
 int band_h2ws_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled);
+int band_h2db_fused_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st,
+                        bool* handled);
 }
 
 namespace {
@@ -1019,10 +938,10 @@ int band_h2_fused_entry(const void* left, const void* right, void* out, float* d
   *handled = false;
   if (disp == nullptr && N * H * W > 0) return fail(SM_EINVAL, "null disparity pointer");
   Args a;
-  bool vec = false;
+  bool vec = false, al4 = false;
   // (the volume check of check_dot_args needs a pointer when only the disparity is wanted)
   int rc = h2_prepare(left, right, out ? out : disp, dtype, N, C, H, W, D, l_strides, r_strides,
-                      &a, &vec);
+                      &a, &vec, &al4);
   if (rc) return rc;
   if (N * H * W == 0) {
     *handled = true;
@@ -1046,6 +965,13 @@ int band_h2_fused_entry(const void* left, const void* right, void* out, float* d
   a.mul = 1.0f / (float)C;
   const bool mean = mode == 1;
   hipStream_t st = as_stream(stream);
+#ifndef SMCV_NO_DB_FUSE  // (diagnostic builds: -DSMCV_NO_DB_FUSE keeps band_h2's FUSE 1 path)
+  if (out != nullptr) {  // volume kept, aligned rows: the double-buffered kernel with the fold
+    bool done = false;
+    rc = band_h2db_fused_run(a, N, mean, al4, st, &done);
+    if (done || rc != SM_OK) return rc;
+  }
+#endif
   return by_tmax(a.pw, [&](auto tm) {
     constexpr int TM = decltype(tm)::value;
     // FUSE 1: volume + disparities; FUSE 2: disparities only -- no shear, no ring, no volume

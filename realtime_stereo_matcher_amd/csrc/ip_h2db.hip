@@ -56,7 +56,9 @@ struct Geo {
 };
 }  // namespace db
 
-template <bool MEAN, int TMAX>
+// FUSE 1: the soft-argmin of the volume is folded from the accumulators before the shear
+// (fused_softargmin, band_common.h) and stored beside it (f-1, volume kept, one D pass).
+template <bool MEAN, int TMAX, int FUSE>
 __global__ __launch_bounds__(db::kThreads, 2) void band_h2db(Args args) {
   using namespace db;
   using G = db::Geo<TMAX>;
@@ -222,6 +224,11 @@ __global__ __launch_bounds__(db::kThreads, 2) void band_h2db(Args args) {
   const int lane_st = rl * H * W + 4 * cl;
 
   auto epilogue_v = [&](const Work& k, bool fast, unsigned buf, auto scale, auto xlt) {
+    // FUSE: the disparity store is issued after the next step's loads and before the chunk
+    // stores, so vm_wait_st's count of younger stores stays a lower bound (the wait also covers it)
+    if constexpr (FUSE == 1)
+      fused_softargmin<TMAX, MEAN, decltype(scale)::value, decltype(xlt)::value, false>(
+          acc, args, k, kL, kR, wave, lr, hh);
     const int x0w = k.x0 + 32 * wave;
     const float mul = args.mul;
     const int kk = -(kL + kR);
@@ -314,16 +321,45 @@ __global__ __launch_bounds__(db::kThreads, 2) void band_h2db(Args args) {
     const float mul = MEAN ? args.mul : 1.0f;
     const float* lrow = L + (int64_t)k.n * ls.n + (int64_t)k.y * ls.h;
     const float* rrow = R + (int64_t)k.n * rs.n + (int64_t)k.y * rs.h;
-    for (int idx = tid; idx < k.Dp * kXT; idx += kThreads) {
-      const int dl = idx / kXT, x = k.x0 + idx % kXT, d = k.dp + dl;
-      if (x >= W) continue;
+    auto cell = [&](int x, int d) {
       float s = 0.f;
       if (x >= d) {
         for (int c = 0; c < cpg; ++c)
           s = __builtin_fmaf(ld1(lrow + (int64_t)c * ls.c + x), ld1(rrow + (int64_t)c * rs.c + x - d), s);
         s *= mul;
       }
-      store_one<float>(out + (((size_t)k.n * D + d) * H + k.y) * W + x, s);
+      return s;
+    };
+    for (int idx = tid; idx < k.Dp * kXT; idx += kThreads) {
+      const int dl = idx / kXT, x = k.x0 + idx % kXT, d = k.dp + dl;
+      if (x >= W) continue;
+      store_one<float>(out + (((size_t)k.n * D + d) * H + k.y) * W + x, cell(x, d));
+    }
+    if constexpr (FUSE == 1) {  // the pixel's soft-argmin from the same exact cells (one D pass)
+      for (int xx = tid; xx < kXT; xx += kThreads) {
+        const int x = k.x0 + xx;
+        if (x >= W) continue;
+        float m = -INFINITY;
+        double s = 0.0, t = 0.0;  // relative to m
+        bool nan = false;
+        for (int d = 0; d < k.Dp; ++d) {
+          const float v = cell(x, k.dp + d);
+          nan |= v != v;
+          if (v > m) {
+            const double f = m == -INFINITY ? 0.0 : (double)expf(m - v);
+            s *= f;
+            t *= f;
+            m = v;
+          }
+          if (m != INFINITY && m != -INFINITY) {
+            const double e = (double)expf(v - m);
+            s += e;
+            t += (double)d * e;
+          }
+        }
+        store_one<float>(args.disp + ((size_t)k.n * H + k.y) * W + x,
+                         (nan || m == INFINITY || m == -INFINITY) ? NAN : (float)(t / s));
+      }
     }
   };
 
@@ -445,14 +481,14 @@ __global__ __launch_bounds__(db::kThreads, 2) void band_h2db(Args args) {
   vm_wait_st(0);  // nothing in flight when the registers die
 }
 
-template <bool MEAN, int TMAX>
+template <bool MEAN, int TMAX, int FUSE>
 int launch_h2db(Args a, int64_t N, hipStream_t st) {
   using G = db::Geo<TMAX>;
   a.tiles = (int)ceil_div(a.W, kXT);
   const int64_t nwork = (int64_t)a.tiles * a.H * N * a.G * a.npass;
   if (nwork > INT32_MAX / 64) return fail(SM_EINVAL, "band kernel: too much work for one launch");
   a.nwork = (int)nwork;
-  auto kern = band_h2db<MEAN, TMAX>;
+  auto kern = band_h2db<MEAN, TMAX, FUSE>;
   static std::atomic<unsigned long long> lds_done{0};
   const int dev = stream_device(st);
   if (int rc = ensure_lds_limit(reinterpret_cast<const void*>(kern), (int)G::SHM, dev, lds_done))
@@ -472,7 +508,26 @@ int band_h2db_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_
   *handled = true;
   auto go = [&](auto tm) {
     constexpr int TM = decltype(tm)::value;
-    return mean ? launch_h2db<true, TM>(a, N, st) : launch_h2db<false, TM>(a, N, st);
+    return mean ? launch_h2db<true, TM, 0>(a, N, st) : launch_h2db<false, TM, 0>(a, N, st);
+  };
+  if (a.pw <= 32) return go(std::integral_constant<int, 2>{});
+  if (a.pw <= 64) return go(std::integral_constant<int, 3>{});
+  if (a.pw <= 128) return go(std::integral_constant<int, 5>{});
+  return go(std::integral_constant<int, 7>{});
+}
+
+// The same kernel with the soft-argmin folded in (FUSE 1): volume and disparity (args.disp) in
+// one pass; one D pass (D <= 192), fp32, aligned rows.
+int band_h2db_fused_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st,
+                        bool* handled) {
+  *handled = false;
+  if (!aligned4 || a.G != 1 || a.pw > 192 || a.npass != 1 || a.out == nullptr ||
+      a.disp == nullptr || a.ws_m != nullptr)
+    return SM_OK;
+  *handled = true;
+  auto go = [&](auto tm) {
+    constexpr int TM = decltype(tm)::value;
+    return mean ? launch_h2db<true, TM, 1>(a, N, st) : launch_h2db<false, TM, 1>(a, N, st);
   };
   if (a.pw <= 32) return go(std::integral_constant<int, 2>{});
   if (a.pw <= 64) return go(std::integral_constant<int, 3>{});

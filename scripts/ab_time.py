@@ -44,6 +44,8 @@ def ops():
                       8, 663552000),
         "cfg2_h2ws": (lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="h2ws"))(*feats((8, 64, 540, 960), torch.float32)),
                       8, 663552000),
+        "cfg2_fused": (lambda: (lambda L, R: lambda: F.inner_product_soft_argmin(L, R, 192, keep_volume=True))(
+            *feats((8, 64, 540, 960), torch.float32)), 8, 665625600),
         "cfg2_fused_nv": (lambda: (lambda L, R: lambda: F.inner_product_soft_argmin(L, R, 192, keep_volume=False))(
             *feats((8, 64, 540, 960), torch.float32)), 8, 267494400),
         "cfg2_regress": (lambda: (lambda v: lambda: F.soft_argmin(v))(torch.randn(8, 192, 540, 960, device="cuda")),
