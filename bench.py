@@ -130,6 +130,10 @@ def kernel_name(cfg, pipeline, algo):
         return {"valu": "dot_volume_valu", "f32": "ip_band_f32", "mfma": "ip_band_f32",
                 "bf16x3": "ip_band_mfma", "h2": "band_h2", "b16": "band_b16",
                 "h2ws": "band_h2ws"}.get(algo, "band_h2db")
+    if pipeline == "fused" and cfg.get("D", 0) <= 192:  # volume kept, one D pass: band_h2db FUSE 1
+        return "band_h2db (fused soft-argmin, volume kept)"
+    if pipeline == "fused-novolume":
+        return "band_h2 (fused soft-argmin, volume-free)"
     return "band_h2 (fused soft-argmin)" if pipeline.startswith("fused") else "band_h2"
 
 
