@@ -226,9 +226,16 @@ __global__ __launch_bounds__(db::kThreads, 2) void band_h2db(Args args) {
   auto epilogue_v = [&](const Work& k, bool fast, unsigned buf, auto scale, auto xlt) {
     // FUSE: the disparity store is issued after the next step's loads and before the chunk
     // stores, so vm_wait_st's count of younger stores stays a lower bound (the wait also covers it)
-    if constexpr (FUSE == 1)
-      fused_softargmin<TMAX, MEAN, decltype(scale)::value, decltype(xlt)::value, false>(
-          acc, args, k, kL, kR, wave, lr, hh);
+    if constexpr (FUSE == 1) {
+      // the sum kernel folds with an explicit x 1.0 (exact): the register allocator then fits
+      // the fold into 256 registers as it does for the mean (368 B of scratch otherwise)
+      Args fa = args;
+      float one = 1.0f;
+      asm volatile("" : "+v"(one));
+      if constexpr (!MEAN) fa.mul = one;
+      fused_softargmin<TMAX, true, decltype(scale)::value, decltype(xlt)::value, false>(
+          acc, fa, k, kL, kR, wave, lr, hh);
+    }
     const int x0w = k.x0 + 32 * wave;
     const float mul = args.mul;
     const int kk = -(kL + kR);

@@ -142,10 +142,8 @@ def check(asm_text):
                         changed = True
         rep = []
         for i, b in enumerate(blocks):  # band_b16 must not spill at all (4 waves per SIMD)
-            # no scratch at all in band_b16, band_h2ws and the volume band_h2db (FUSE 0); the
-            # fused band_h2db may spill (its waits stay correct: younger ops only add to vmcnt)
-            no_scr = ("8band_b16" in name or "9band_h2ws" in name or
-                      re.search(r"9band_h2dbILb[01]ELi\d+ELi0E", name) is not None)
+            # no scratch at all in band_b16, band_h2db (volume and fused) and band_h2ws
+            no_scr = "8band_b16" in name or "9band_h2db" in name or "9band_h2ws" in name
             transfer(b, ins_state[i], rep, no_scratch=no_scr)
         bad += [f"{name}:{r}" for r in rep]
     return bad
