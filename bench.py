@@ -86,7 +86,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=None,
                     help="pairs per GPU per step (weak scaling; overrides --global-batch)")
     ap.add_argument("--chunk", type=int, default=None, help="pairs per kernel launch")
-    ap.add_argument("--algo", default="auto", choices=["auto", "h2", "h2db", "h2ws", "b16", "bf16x3", "f32", "mfma", "valu"],
+    ap.add_argument("--algo", default="auto", choices=["auto", "sp", "h2", "h2db", "f32", "mfma", "valu"],
                     help="cfg2 volume kernel of --pipeline separate")
     ap.add_argument("--pipeline", default="separate",
                     choices=["separate", "fused", "fused-novolume", "interweave"])
@@ -126,10 +126,11 @@ def kernel_name(cfg, pipeline, algo):
     if cfg["op"] == "groupwise":
         return "band_h2 (NGHWD, bf16)"
     if cfg["op"] in ("inner_product", "correlation") and pipeline == "separate":
-        # fp32 aligned rows: the double-buffered band kernel (AUTO); algos pick the others
+        # fp32 aligned rows with C = 16 or 64 and > 64 disparities per pass (cfg2, cfg4): the
+        # software-pipelined band kernel (AUTO); other shapes the double-buffered one
+        sp_shape = cfg["C"] in (16, 64) and cfg["D"] > 64
         return {"valu": "dot_volume_valu", "f32": "ip_band_f32", "mfma": "ip_band_f32",
-                "bf16x3": "ip_band_mfma", "h2": "band_h2", "b16": "band_b16",
-                "h2ws": "band_h2ws"}.get(algo, "band_h2db")
+                "h2": "band_h2", "sp": "band_sp" if sp_shape else "band_h2db"}.get(algo, "band_h2db")
     if pipeline == "fused" and cfg.get("D", 0) <= 192:  # volume kept, one D pass: band_h2db FUSE 1
         return "band_h2db (fused soft-argmin, volume kept)"
     if pipeline == "fused-novolume":
@@ -144,8 +145,6 @@ def arithmetic(cfg, pipeline, algo):
         return "exact bf16 products on v_mfma_f32_32x32x16_bf16, fp32 accumulate, x 1/(C/G)"
     if cfg["op"] == "inner_product" and pipeline == "separate" and algo in ("f32", "mfma"):
         return "exact fp32 products on v_mfma_f32_16x16x4_f32"
-    if cfg["op"] == "inner_product" and pipeline == "separate" and algo == "bf16x3":
-        return "fp32-accurate 3-way bf16 split on bf16 MFMA"
     if cfg["op"] == "inner_product" and pipeline == "separate" and algo == "valu":
         return "fp32 FMA (VALU)"
     return ARITH_SPLIT + ("; soft-argmin online in fp32/fp64" if pipeline.startswith("fused") else

@@ -49,17 +49,21 @@ enum sm_ip_algo {
   SM_IP_AUTO = 0,        /* library default for the shape/dtype */
   SM_IP_VALU = 1,        /* fp32 VALU, LDS-staged right window reused across the D sweep */
   SM_IP_MFMA_F32 = 2,    /* banded C-contraction on v_mfma_f32_16x16x4_f32 (exact fp32 fma) */
-  SM_IP_MFMA_BF16X3 = 3, /* banded C-contraction on bf16 MFMA over an exact 3-way bf16 split */
+  /* 3: reserved (the bf16 3-way split kernel, retired in round 4: slower than MFMA_H2) */
   /* 4: reserved (a retired warp-specialised variant of the bf16 split) */
   SM_IP_MFMA_H2 = 5,     /* banded contraction on 32x32x16 MFMA, two workgroups per CU, every wave
-                            loads, stages, multiplies and stores (the default) */
+                            loads, stages, multiplies and stores (the default for fp16 / bf16
+                            features and for fp32 rows that are not 4-element aligned) */
   /* 6: reserved (a retired warp-specialised variant, removed in round 3) */
-  SM_IP_MFMA_B16 = 7,    /* the same contraction re-tiled on 16x16x32 MFMA: 16-pixel waves, four
-                            waves per SIMD (fp32, 4-element aligned rows; other shapes: MFMA_H2) */
+  /* 7: reserved (16-pixel waves on 16x16x32 MFMA, retired in round 4: slower than MFMA_H2DB) */
   SM_IP_MFMA_H2DB = 8,   /* MFMA_H2 with double-buffered planes: the next step is staged inside
-                            the current step's MFMA phase (fp32, aligned rows; else MFMA_H2) */
-  SM_IP_MFMA_H2WS = 9    /* MFMA_H2DB with the volume stores moved to dedicated store waves fed
-                            through an LDS queue (fp32, aligned rows; else MFMA_H2) */
+                            the current step's MFMA phase (fp32, aligned rows; else MFMA_H2; the
+                            fallback of MFMA_SP and of AUTO) */
+  /* 9: reserved (store waves fed through an LDS queue, retired in round 4: slower) */
+  SM_IP_MFMA_SP = 10     /* software-pipelined band kernel: one workgroup per CU, two accumulator
+                            sets, the previous segment's shear and stores spread over the current
+                            segment's steps (fp32, aligned rows, C = 16 or 64, D in 65..192 per
+                            pass; other shapes: MFMA_H2DB) */
 };
 
 /* Library version (major*10000 + minor*100 + patch). */

@@ -14,7 +14,7 @@ SM_F32, SM_F16, SM_BF16 = 0, 1, 2
 SM_OK, SM_EINVAL, SM_EDTYPE, SM_ELAUNCH, SM_EUNSUPPORTED = 0, -1, -2, -3, -4
 SM_ARGMIN, SM_ARGMAX = 0, 1
 SM_REGRESS_SOFTMAX, SM_REGRESS_PRESOFTMAXED, SM_REGRESS_OUT_F32 = 0, 1, 2
-SM_IP_AUTO, SM_IP_VALU, SM_IP_MFMA_F32, SM_IP_MFMA_BF16X3, SM_IP_MFMA_H2, SM_IP_MFMA_B16, SM_IP_MFMA_H2DB, SM_IP_MFMA_H2WS = 0, 1, 2, 3, 5, 7, 8, 9
+SM_IP_AUTO, SM_IP_VALU, SM_IP_MFMA_F32, SM_IP_MFMA_H2, SM_IP_MFMA_H2DB, SM_IP_MFMA_SP = 0, 1, 2, 5, 8, 10
 
 _p = ctypes.c_void_p
 _i = ctypes.c_int

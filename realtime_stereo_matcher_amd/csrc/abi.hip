@@ -6,9 +6,6 @@ int dot_volume_valu_entry(const void* left, const void* right, void* out, int dt
                           int64_t C, int64_t H, int64_t W, int64_t D, int64_t G,
                           const int64_t* l_strides, const int64_t* r_strides, int mode,
                           void* stream);
-int band_mfma_entry(const void* left, const void* right, void* out, int dtype, int64_t N, int64_t C,
-                    int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
-                    const int64_t* r_strides, int mode, void* stream);
 int band_f32_entry(const void* left, const void* right, void* out, int dtype, int64_t N,
                    int64_t C, int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
                    const int64_t* r_strides, int mode, void* stream, bool* handled);
@@ -72,13 +69,12 @@ extern "C" int sm_cv_inner_product_ex(const void* left, const void* right, void*
     }
     case SM_IP_AUTO:  // the two-plane fp16 band kernel; odd shapes: the exact VALU kernel
     case SM_IP_MFMA_H2:
-    case SM_IP_MFMA_B16:
     case SM_IP_MFMA_H2DB:
-    case SM_IP_MFMA_H2WS: {
+    case SM_IP_MFMA_SP: {
       bool handled = false;
-      // AUTO: fp32 aligned rows take the double-buffered band (band_h2db), the rest band_h2
-      const int variant = algo == SM_IP_MFMA_B16    ? 1
-                          : algo == SM_IP_MFMA_H2WS ? 3
+      // AUTO: fp32 aligned rows take the double-buffered band (band_h2db), the rest band_h2;
+      // SP: the software-pipelined band (band_sp), shapes it does not take band_h2db
+      const int variant = algo == SM_IP_MFMA_SP ? 4
                           : (algo == SM_IP_MFMA_H2DB || algo == SM_IP_AUTO) ? 2
                                                     : 0;
       int rc = band_h2_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
@@ -87,9 +83,6 @@ extern "C" int sm_cv_inner_product_ex(const void* left, const void* right, void*
       return dot_volume_valu_entry(left, right, out, dtype, N, C, H, W, D, 1, l_strides,
                                    r_strides, 0, stream);
     }
-    case SM_IP_MFMA_BF16X3:
-      return band_mfma_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
-                             stream);
     case SM_IP_VALU:
       return dot_volume_valu_entry(left, right, out, dtype, N, C, H, W, D, 1, l_strides,
                                    r_strides, 0, stream);

@@ -1,4 +1,5 @@
-// Helpers shared by the band cost-volume kernels (ip_h2.hip: band_h2; ip_b16.hip: band_b16):
+// Helpers shared by the band cost-volume kernels (ip_h2.hip: band_h2; ip_h2db.hip: band_h2db;
+// ip_sp.hip: band_sp):
 // operand typedefs, the plane swizzle, the work decomposition, LDS accessors, the hand-counted
 // feature loads and their vmcnt wait, the output stores and the fp32 two-plane split.
 #pragma once
@@ -213,7 +214,7 @@ __device__ __forceinline__ void split_pair(float a, float b, float sc, unsigned&
 // exponent e with x = f 2^e, f in [0.5, 1) (x > 0 finite)
 __device__ __forceinline__ int exp_of(float x) { return __builtin_amdgcn_frexp_expf(x); }
 
-// The persistent grid's schedule (band_h2, band_h2db, band_b16).  Workgroups b and b+8 share an
+// The persistent grid's schedule (band_h2, band_h2db, band_sp).  Workgroups b and b+8 share an
 // XCD, and each XCD group walks a contiguous range of row segments, so neighbouring segments of
 // a row run on one XCD at the same time and share its L2 for the right window.  Item i of a
 // workgroup is segment j = gi + (i / npass) gsz of its group's range, pass i % npass: the D

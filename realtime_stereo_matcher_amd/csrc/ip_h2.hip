@@ -801,9 +801,8 @@ int check_dot_args(const void* left, const void* right, const void* out, int dty
                    const int64_t* r_strides, Strides4* ls, Strides4* rs);
 
 namespace h2band {
-int band_b16_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled);
 int band_h2db_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled);
-int band_h2ws_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled);
+int band_sp_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled);
 int band_h2db_fused_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st,
                         bool* handled);
 }
@@ -874,13 +873,16 @@ int band_h2_entry(const void* left, const void* right, void* out, int dtype, int
   const bool mean = mode == 1;
   a.mul = 1.0f / (float)C;
   hipStream_t st = as_stream(stream);
-  // fp32 with aligned rows: variant 1 the four-waves-per-SIMD tiling (band_b16), variant 2 the
-  // double-buffered pipeline (band_h2db), variant 3 the store-decoupled pipeline (band_h2ws); other shapes (and variant 0) run band_h2
+  // fp32 with aligned rows: variant 4 the software-pipelined kernel (band_sp; the shapes it does
+  // not take fall through to band_h2db), variant 2 the double-buffered pipeline (band_h2db);
+  // other shapes (and variant 0) run band_h2
   if (variant != 0 && dtype == SM_F32) {
     bool done = false;
-    rc = variant == 1   ? band_b16_run(a, N, mean, al4, st, &done)
-         : variant == 3 ? band_h2ws_run(a, N, mean, al4, st, &done)
-                        : band_h2db_run(a, N, mean, al4, st, &done);
+    if (variant == 4) {  // the software-pipelined kernel; shapes it does not take: band_h2db
+      rc = band_sp_run(a, N, mean, al4, st, &done);
+      if (done || rc != SM_OK) return rc;
+    }
+    rc = band_h2db_run(a, N, mean, al4, st, &done);
     if (done || rc != SM_OK) return rc;
   }
   SM_DISPATCH_DTYPE(dtype, T0, {

@@ -42,6 +42,8 @@ def ops():
                      8, 663552000),
         "cfg2_h2db": (lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="h2db"))(*feats((8, 64, 540, 960), torch.float32)),
                       8, 663552000),
+        "cfg2_sp": (lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="sp"))(*feats((8, 64, 540, 960), torch.float32)),
+                    8, 663552000),
         "cfg2_h2ws": (lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="h2ws"))(*feats((8, 64, 540, 960), torch.float32)),
                       8, 663552000),
         "cfg2_fused": (lambda: (lambda L, R: lambda: F.inner_product_soft_argmin(L, R, 192, keep_volume=True))(

@@ -8,7 +8,9 @@ kernel relies on two properties of the generated code, checked here for every in
   2. no wave ends (s_endpgm) with such a load still in flight (the L2 touches included);
   3. no `flat_*` memory instruction exists (flat ops count in vmcnt out of order, which would
      break the `vmcnt(4 (T-1))` wait that lets the output stores stay in flight);
-  4. band_b16 (ip_b16.hip) has no scratch access at all: a spill reload counts in vmcnt and
+  4. band_h2db (ip_h2db.hip) and band_sp (ip_sp.hip) have no scratch access at all: a spill
+     reload counts in vmcnt (band_sp's loads are compiler-tracked; the other checks find no
+     inline-asm loads in it, and the scratch check is what applies there) and
      would wait for the feature loads in flight.
 A may-pending dataflow over the kernel's basic blocks carries each load to every instruction it
 can reach before a vmcnt wait.
@@ -24,8 +26,7 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "realtime_stereo_matcher_amd", "csrc")
-SRCS = [os.path.join(CSRC, "ip_h2.hip"), os.path.join(CSRC, "ip_b16.hip"), os.path.join(CSRC, "ip_h2db.hip"),
-        os.path.join(CSRC, "ip_h2ws.hip")]
+SRCS = [os.path.join(CSRC, "ip_h2.hip"), os.path.join(CSRC, "ip_h2db.hip"), os.path.join(CSRC, "ip_sp.hip")]
 
 
 def regs(tok):
@@ -42,7 +43,7 @@ def kernels(asm_text):
     only those loads are hand-counted (the compiler waits for its own)."""
     out, cur, in_asm = [], None, False
     for ln, line in enumerate(asm_text.splitlines(), 1):
-        if re.match(r"^_ZN4smcv6h2band(7band_h2|8band_b16|9band_h2db|9band_h2ws).*:", line):
+        if re.match(r"^_ZN4smcv6h2band(7band_h2|9band_h2db|7band_sp).*:", line):
             cur = (line.split(":")[0], [])
             out.append(cur)
             continue
@@ -141,9 +142,9 @@ def check(asm_text):
                         ins_state[j] |= out
                         changed = True
         rep = []
-        for i, b in enumerate(blocks):  # band_b16 must not spill at all (4 waves per SIMD)
-            # no scratch at all in band_b16, band_h2db (volume and fused) and band_h2ws
-            no_scr = "8band_b16" in name or "9band_h2db" in name or "9band_h2ws" in name
+        for i, b in enumerate(blocks):
+            # no scratch at all in band_h2db (volume and fused) and band_sp
+            no_scr = "9band_h2db" in name or "7band_sp" in name
             transfer(b, ins_state[i], rep, no_scratch=no_scr)
         bad += [f"{name}:{r}" for r in rep]
     return bad
@@ -152,9 +153,9 @@ def check(asm_text):
 def main():
     args = sys.argv[1:]
     srcs = SRCS
-    if "--stamps" in args:  # the diagnostic driver (scripts/ip_stamps.hip) instead
+    if "--stamps" in args:  # the round-3 diagnostic driver (scripts/experimental/ip_stamps.hip) instead
         args.remove("--stamps")
-        srcs = [os.path.join(ROOT, "scripts", "ip_stamps.hip")]
+        srcs = [os.path.join(ROOT, "scripts", "experimental", "ip_stamps.hip")]
         args.append("-DSMCV_STAMPS")
     bad, n = [], 0
     for src in srcs:

@@ -3,7 +3,7 @@
 #   bash scripts/gpu_h2.sh TAG [pytest -k expr] [ops]
 cd "$GRAFT_REPO_ROOT" || exit 1
 TAG=${1:-h2}; K=${2:-"inner_product or correlation or cfg2 or cfg4 or noncontig or zero"}
-OPS=${3:-inner_product_h2_cfg2,inner_product_bf16x3_cfg2,correlation_cfg4_pair,soft_argmin_cfg2}
+OPS=${3:-inner_product_h2_cfg2,correlation_cfg4_pair,soft_argmin_cfg2}
 OUT=gpurun_out/$TAG; mkdir -p "$OUT"; export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -k "$K" > "$OUT/pytest_gpu.log" 2>&1
 rc=$?; echo "pytest rc=$rc" >> "$OUT/pytest_gpu.log"

@@ -20,7 +20,6 @@ def feats(shape, dtype):
 OPS = {
     "inner_product_mfma_cfg2": lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="mfma"))(*feats((1, 64, 540, 960), torch.float32)),
     "inner_product_h2_cfg2": lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="h2"))(*feats((1, 64, 540, 960), torch.float32)),
-    "inner_product_bf16x3_cfg2": lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="bf16x3"))(*feats((1, 64, 540, 960), torch.float32)),
     "inner_product_valu_cfg2": lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="valu"))(*feats((1, 64, 540, 960), torch.float32)),
     "soft_argmin_cfg2": lambda: (lambda v: lambda: F.soft_argmin(v))(torch.randn(1, 192, 540, 960, device="cuda")),
     "groupwise_bf16_cfg3": lambda: (lambda L, R: lambda: F.groupwise_volume(L, R, 8, 192))(*feats((1, 256, 540, 960), torch.bfloat16)),

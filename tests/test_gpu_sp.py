@@ -1,0 +1,175 @@
+"""GPU parity of the software-pipelined band kernel (algo "sp", csrc/ip_sp.hip) against the CPU
+oracle, on the shapes it takes (fp32, 4-element aligned rows, C = 16 or 64, D > 64 per pass),
+including the bench's own launch shapes (cfg2: 8 pairs per launch; cfg4: 4 pairs).
+
+Reference op: TorchInnerProductCost.forward (cost_volume/inner_product.py:11-42) and
+make_correlation_volume (model/mobile_disp_net_c.py:188-205).  Tolerance: 1e-4 absolute for
+fp32 volumes (north star), bit-exact for integer-valued features, relative 1e-5 of
+sum_c |L||R| for scaled features.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import stereo_oracle as O
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to("cuda")
+
+
+def host(t):
+    return t.float().cpu().numpy()
+
+
+def _feats(seed, shape, kind="normal"):
+    rng = np.random.default_rng(seed)
+    if kind == "int":
+        return (rng.integers(-8, 9, size=shape).astype(np.float32),
+                rng.integers(-8, 9, size=shape).astype(np.float32))
+    return rng.standard_normal(shape, dtype=np.float32), rng.standard_normal(shape, dtype=np.float32)
+
+
+# (N, C, H, W, D): every segment pattern -- the 64-pixel last tile of a 960 row, rows shorter
+# than one segment, W = 4, odd item counts per workgroup, D one disparity past a block, two
+# balanced D passes of 128 (D = 256), D > W
+SP_SHAPES = [(1, 64, 3, 512, 192), (2, 64, 5, 260, 100), (3, 64, 2, 132, 128), (2, 64, 3, 960, 191),
+             (1, 64, 2, 16, 96), (1, 64, 1, 4, 80), (1, 16, 4, 388, 192), (1, 16, 3, 1000, 256),
+             (2, 16, 2, 200, 65), (1, 64, 2, 64, 192), (5, 16, 1, 900, 160)]
+
+
+@pytest.mark.parametrize("shape", SP_SHAPES, ids=[str(s) for s in SP_SHAPES])
+def test_sp_inner_product_and_correlation(shape):
+    from realtime_stereo_matcher_amd import functional as F
+
+    n, c, h, w, D = shape
+    l, r = _feats(hash(shape) % 997, (n, c, h, w))
+    got = host(F.inner_product_volume(dev(l), dev(r), D, algo="sp"))
+    np.testing.assert_allclose(got, O.inner_product(l, r, D), atol=TOL, rtol=0)
+    # identical to the double-buffered kernel's volume up to fp32 summation order: both use the
+    # same split; compare loosely, and exactly on integer-valued features
+    li, ri = _feats(7, (n, c, h, w), "int")
+    np.testing.assert_array_equal(host(F.inner_product_volume(dev(li), dev(ri), D, algo="sp")),
+                                  O.inner_product(li, ri, D))
+    corr = host(F.correlation_volume(dev(l), dev(r), D))  # AUTO (sp once it is the default)
+    np.testing.assert_allclose(corr, O.correlation_mean(l, r, D), atol=TOL, rtol=0)
+
+
+def _cell_norm(l, r, D):
+    return O.inner_product(np.abs(l), np.abs(r), D)
+
+
+@pytest.mark.parametrize("scale", [1e-15, 1e-6, 1e6, 1e15])
+def test_sp_feature_scales(scale):
+    """Uniformly tiny or huge features: the first segment is recomputed with a new power-of-two
+    scale (the pipeline restart), later ones carry it."""
+    from realtime_stereo_matcher_amd import functional as F
+
+    l, r = _feats(21, (1, 64, 3, 512))
+    l, r = (l * scale).astype(np.float32), (r * scale).astype(np.float32)
+    got = host(F.inner_product_volume(dev(l), dev(r), 192, algo="sp"))
+    err = np.abs(got - O.inner_product(l, r, 192))
+    assert (err <= 1e-5 * _cell_norm(l, r, 192) + 1e-37).all()
+
+
+def test_sp_mixed_scales():
+    """Scale changing from row to row and pixel to pixel: restarts and carried scales mixed
+    with the drain of the previous segment (its own scale)."""
+    from realtime_stereo_matcher_amd import functional as F
+
+    rng = np.random.default_rng(5)
+    n, c, h, w, D = 2, 64, 6, 640, 160
+    l, r = _feats(22, (n, c, h, w))
+    l = (l * 10.0 ** rng.uniform(-8, 8, (n, 1, h, 1)) * 10.0 ** rng.uniform(-2, 2, (n, 1, h, w))).astype(np.float32)
+    r = (r * 10.0 ** rng.uniform(-8, 8, (n, 1, h, 1)) * 10.0 ** rng.uniform(-2, 2, (n, 1, h, w))).astype(np.float32)
+    got = host(F.inner_product_volume(dev(l), dev(r), D, algo="sp"))
+    err = np.abs(got - O.inner_product(l, r, D))
+    bound = 1e-5 * _cell_norm(l, r, D) + 1e-30
+    assert (err <= bound).all(), float((err / bound).max())
+
+
+@pytest.mark.parametrize("c", [16, 64])
+def test_sp_nonfinite(c):
+    """+-inf features take the exact path; NaN reaches the band (max|x| does not see it) and the
+    x < d cells are still forced to 0; the drained neighbours are unaffected."""
+    from realtime_stereo_matcher_amd import functional as F
+
+    l, r = _feats(23, (1, c, 4, 512))
+    l[0, 5, 0, 130] = np.inf
+    l[0, 0, 1, 7] = -np.inf
+    r[0, 3, 1, 100] = np.nan
+    r[0, 9, 2, 3] = np.inf
+    l[0, 2, 3, 1] = np.nan  # NaN in L next to the x < d triangle
+    r[0, 1, 3, 0] = np.nan  # NaN at R pixel 0: the pad groups of the row read it
+    D = 128
+    got = host(F.inner_product_volume(dev(l), dev(r), D, algo="sp"))
+    want = O.inner_product(l, r, D)
+    np.testing.assert_array_equal(np.isnan(got), np.isnan(want))
+    np.testing.assert_array_equal(np.isposinf(got), np.isposinf(want))
+    np.testing.assert_array_equal(np.isneginf(got), np.isneginf(want))
+    fin = np.isfinite(want)
+    np.testing.assert_allclose(got[fin], want[fin], atol=TOL, rtol=0)
+
+
+def test_sp_strided_inputs():
+    """Channel- and batch-strided views (rows contiguous) go through the ABI strides."""
+    from realtime_stereo_matcher_amd import functional as F
+
+    l, r = _feats(9, (2, 128, 3, 320))
+    L, R = dev(l)[:, ::2], dev(r)[:, 1::2]  # C = 64 with channel stride 2 H W
+    got = host(F.inner_product_volume(L, R, 192, algo="sp"))
+    np.testing.assert_allclose(got, O.inner_product(l[:, ::2], r[:, 1::2], 192), atol=TOL, rtol=0)
+
+
+def _check_rows(vol, ln, rn, D, rows, mean=False):
+    for n in range(vol.shape[0]):
+        for y in rows:
+            fn = O.correlation_mean if mean else O.inner_product
+            ref = fn(ln[n:n + 1, :, y:y + 1], rn[n:n + 1, :, y:y + 1], D)
+            np.testing.assert_allclose(host(vol[n:n + 1, :, y:y + 1]), ref, atol=TOL, rtol=0,
+                                       err_msg=f"pair {n} row {y}")
+
+
+def test_sp_cfg2_bench_launch_shape():
+    """The bench's launch: 8 cfg2 pairs (8x64x540x960 fp32, D = 192) in ONE launch.  Rows of
+    EVERY pair (first, last and the pair boundaries of the persistent schedule) against the
+    oracle, the x < d triangle exactly zero, and the soft-argmin of every sampled row."""
+    from realtime_stereo_matcher_amd import functional as F
+
+    g = torch.Generator(device="cuda").manual_seed(3)
+    L = torch.randn(8, 64, 540, 960, device="cuda", generator=g)
+    R = torch.randn(8, 64, 540, 960, device="cuda", generator=g)
+    vol = F.inner_product_volume(L, R, 192, algo="sp")
+    disp = F.soft_argmin(vol)
+    torch.cuda.synchronize()
+    ln, rn = host(L), host(R)
+    _check_rows(vol, ln, rn, 192, (0, 1, 270, 538, 539))
+    for n in range(8):
+        got = host(vol[n:n + 1, :, 100:101])
+        np.testing.assert_allclose(host(disp[n:n + 1, :, 100:101]).reshape(-1),
+                                   O.softargmin(got).reshape(-1), atol=TOL, rtol=0)
+    tri = torch.arange(960, device="cuda")[None, :] < torch.arange(192, device="cuda")[:, None]
+    for n in range(8):
+        assert not vol[n].permute(1, 0, 2)[:, tri].any()
+
+
+def test_sp_cfg4_bench_launch_shape():
+    """The bench's cfg4 launch: 4 pairs of 16x1080x1920 fp32, correlation D = 256 (two passes of
+    128 per segment) in one launch; rows of every pair against the oracle."""
+    from realtime_stereo_matcher_amd import functional as F
+
+    g = torch.Generator(device="cuda").manual_seed(4)
+    L = torch.randn(4, 16, 1080, 1920, device="cuda", generator=g)
+    R = torch.randn(4, 16, 1080, 1920, device="cuda", generator=g)
+    vol = F.correlation_volume(L, R, 256)
+    torch.cuda.synchronize()
+    _check_rows(vol, host(L), host(R), 256, (0, 541, 1079), mean=True)

@@ -26,12 +26,3 @@ def test_h2_indexing_replay():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "check_h2_bounds.py")],
                        capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
-
-
-def test_b16_ring_replay():
-    """band_b16's 2-slot shear ring: every chunk readout sees exactly its (d, x) cells, ring writes
-    at most 2-way (free for ds_write_b32), readouts and 16x16x32 fragment reads conflict-free."""
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "check_b16_ring.py")],
-                       capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
-    assert "ring writes 2-way, readouts 1-way, fragment reads 1-way" in r.stdout
