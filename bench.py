@@ -270,6 +270,30 @@ def check_numerics(cfg, a, L, R, last):
         out["mean_abs_err_disparity"] = sum(mean_d) / len(mean_d)
         out["disparity_ok"] = bool(out["mean_abs_err_disparity"] <= 1e-4 and
                                    out["max_abs_err_disparity"] <= max(out["torch_fp32_disparity_dev"], 1e-4))
+    # one row of EVERY pair of the last launch (a different row per pair) against the fp64
+    # oracle: the whole persistent-grid launch, not only its first pair
+    if cfg["op"] in ("inner_product", "correlation", "groupwise") and vol is not None:
+        pairs, worst_v, worst_d = [], 0.0, 0.0
+        for j in range(vol.shape[0]):
+            y = (37 * j + 11) % H
+            ly = host(L[s0 + j:s0 + j + 1, :, y:y + 1].float())
+            ry = host(R[s0 + j:s0 + j + 1, :, y:y + 1].float())
+            if cfg["op"] == "groupwise":
+                ref = O.groupwise(ly, ry, cfg["G"], D).astype(np.float64)
+            else:
+                ref = (O.inner_product(ly, ry, D) if cfg["op"] == "inner_product"
+                       else O.correlation_mean(ly, ry, D)).astype(np.float64)
+            worst_v = max(worst_v, float(np.abs(host(vol[j:j + 1, :, y:y + 1]).astype(np.float64) - ref).max()))
+            if disp is not None:
+                got_v = host(vol[j:j + 1, :, y:y + 1])
+                worst_d = max(worst_d, float(np.abs(host(disp[j:j + 1, :, y:y + 1]).astype(np.float64)
+                                                    - O.softargmin(got_v)).max()))
+            pairs.append([s0 + j, y])
+        out["all_pairs_checked"] = pairs
+        out["all_pairs_max_abs_err_volume"] = worst_v
+        if disp is not None:
+            # the regression of each sampled volume row against its fp64 soft-argmin
+            out["all_pairs_max_abs_err_regression"] = worst_d
     out["tolerance"] = 0.0 if cfg["op"] == "concat" else 1e-4
     return out
 

@@ -211,6 +211,32 @@ __device__ __forceinline__ void split_pair(float a, float b, float sc, unsigned&
       : "v"(a), "v"(b), "v"(sc));
 }
 
+// split_pair for four pairs at once (one pixel's 8 channels -> 16 B of h, 16 B of m), ordered
+// for instruction-level parallelism: each write depends on one issued four instructions earlier
+// (split_pair's four are one dependent chain, which a lone wave on its SIMD waits out).
+__device__ __forceinline__ void split_quad(const float (&x)[8], float sc, uint4& h, uint4& m) {
+  asm("v_fma_mixlo_f16 %0, %8, %16, 0\n\t"
+      "v_fma_mixlo_f16 %1, %10, %16, 0\n\t"
+      "v_fma_mixlo_f16 %2, %12, %16, 0\n\t"
+      "v_fma_mixlo_f16 %3, %14, %16, 0\n\t"
+      "v_fma_mixhi_f16 %0, %9, %16, 0\n\t"
+      "v_fma_mixhi_f16 %1, %11, %16, 0\n\t"
+      "v_fma_mixhi_f16 %2, %13, %16, 0\n\t"
+      "v_fma_mixhi_f16 %3, %15, %16, 0\n\t"
+      "v_fma_mixlo_f16 %4, %8, %16, -%0 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixlo_f16 %5, %10, %16, -%1 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixlo_f16 %6, %12, %16, -%2 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixlo_f16 %7, %14, %16, -%3 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %4, %9, %16, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %5, %11, %16, -%1 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %6, %13, %16, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %7, %15, %16, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(h.x), "=&v"(h.y), "=&v"(h.z), "=&v"(h.w), "=&v"(m.x), "=&v"(m.y), "=&v"(m.z),
+        "=&v"(m.w)
+      : "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), "v"(x[7]),
+        "v"(sc));
+}
+
 // exponent e with x = f 2^e, f in [0.5, 1) (x > 0 finite)
 __device__ __forceinline__ int exp_of(float x) { return __builtin_amdgcn_frexp_expf(x); }
 

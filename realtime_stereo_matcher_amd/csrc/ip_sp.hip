@@ -38,6 +38,9 @@
 // staging into b, and the staging into !b before the next step's fragment reads.
 #include "band_common.h"
 
+#ifndef SMCV_SP_ABLATE
+#define SMCV_SP_ABLATE 0  // diagnostics only (scripts/build_variants.py): 1 no drain stages, 2 no
+#endif                    // staging, 4 feature loads from one line, 8 no MFMA, 16 no barrier
 #ifndef SMCV_SP_SETS
 #define SMCV_SP_SETS 4  // feature-load register sets (loads issued SETS - 1 steps ahead)
 #endif
@@ -129,11 +132,12 @@ __global__ __launch_bounds__(sp::kThreads, 1) void band_sp(Args args) {
   auto load = [&](int set, const Work& k, int ks) __attribute__((always_inline)) {
     const int px = isR ? k.js + 4 * g : k.x0 + 4 * g - G::RW;
     okp[set] = active && px >= 0 && px < W;
-    const int pxc = min(max(px, 0), W - 4);  // pad groups: the nearest valid group
+    int pxc = min(max(px, 0), W - 4);  // pad groups: the nearest valid group
+    if constexpr (SMCV_SP_ABLATE & 4) pxc = 0;
     const float* p = (isR ? R + (int64_t)k.n * rs.n + (int64_t)k.y * rs.h
                           : L + (int64_t)k.n * ls.n + (int64_t)k.y * ls.h) +
-                     pxc + (int64_t)(ks * kKC + 8 * ch) * cs;
-    int64_t csl = cs;
+                     pxc + (SMCV_SP_ABLATE & 4 ? 0 : (int64_t)(ks * kKC + 8 * ch) * cs);
+    int64_t csl = SMCV_SP_ABLATE & 4 ? 0 : cs;
     asm volatile("" : "+v"(csl));
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
@@ -147,6 +151,7 @@ __global__ __launch_bounds__(sp::kThreads, 1) void band_sp(Args args) {
   // Staging of one step into plane buffer `buf` (byte offset), in pieces: piece 0 tracks
   // max|x| and sets the scale; pieces 1-4 split pixel p = piece-1 into the h and m planes.
   auto put_piece = [&](int set, int piece, unsigned buf) __attribute__((always_inline)) {
+    if constexpr (SMCV_SP_ABLATE & 2) return;
     f32x4v(&sv_)[8] = sv[set];
     if (piece == 0) {
       float m0 = 0.f, m1 = 0.f;
@@ -163,10 +168,9 @@ __global__ __launch_bounds__(sp::kThreads, 1) void band_sp(Args args) {
     unsigned o0 = buf + (unsigned)swz(4 * g, ch);
     asm volatile("" : "+v"(o0));
     uint4 wh, wm;
-    split_pair(sv_[0][p], sv_[1][p], sc, wh.x, wm.x);
-    split_pair(sv_[2][p], sv_[3][p], sc, wh.y, wm.y);
-    split_pair(sv_[4][p], sv_[5][p], sc, wh.z, wm.z);
-    split_pair(sv_[6][p], sv_[7][p], sc, wh.w, wm.w);
+    const float xs[8] = {sv_[0][p], sv_[1][p], sv_[2][p], sv_[3][p],
+                         sv_[4][p], sv_[5][p], sv_[6][p], sv_[7][p]};
+    split_quad(xs, sc, wh, wm);
     const unsigned off = active ? o0 ^ (32u * p) : (unsigned)G::DUMMY;  // (no branch)
     *reinterpret_cast<uint4*>(smem + off) = wh;
     *reinterpret_cast<uint4*>(smem + G::PLANE + off) = wm;
@@ -211,6 +215,7 @@ __global__ __launch_bounds__(sp::kThreads, 1) void band_sp(Args args) {
   int p_kk = 0;
   bool p_special = false;  // scaled (kk != 0) or holding cells x < d (js < 0)
   int p_bytes = 0;        // 0x80000000 (valid) or 0 (every store dropped)
+  bool p_full = false;    // the whole 128-pixel segment and all DMAX disparities are stored
   float* p_ob = static_cast<float*>(args.out);  // (n, dp, y, x0w) of the drained segment
   f32x4v vp[4];           // one chunk's readout, stored in the next stage
 
@@ -285,20 +290,29 @@ __global__ __launch_bounds__(sp::kThreads, 1) void band_sp(Args args) {
     asm volatile("" : "+v"(rr), "+v"(cc));
     const unsigned q8 = (unsigned)(8 * plane_stride * 4);
     const unsigned lo = (unsigned)(rr * plane_stride * 4 + 16 * cc);
-    const bool xok = pw.x0 + 32 * wave + 4 * cc < W;
+    if (p_full) {  // every cell of the segment is inside the volume
 #pragma unroll
-    for (int qq = 0; qq < 4; ++qq) {
-      const int dl = 32 * a + 8 * qq + rr;
-      const bool ok = xok && dl < pw.Dp;
-      const unsigned voff = ok ? lo + (unsigned)qq * q8 : 0x80000000u;
-      __builtin_amdgcn_raw_buffer_store_b128(
-          __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, vp[qq]), rsrc, voff, 0,
-          SMCV_NT_STORE ? 2 : 0);
+      for (int qq = 0; qq < 4; ++qq)
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, vp[qq]), rsrc,
+            lo + (unsigned)qq * q8, 0, SMCV_NT_STORE ? 2 : 0);
+    } else {
+      // masked lanes: the offset's top bit set (out of range; no select, which the compiler
+      // would turn into branches around the stores)
+      const unsigned xbad = (unsigned)(pw.x0 + 32 * wave + 4 * cc >= W) << 31;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const unsigned bad = xbad | ((unsigned)(32 * a + 8 * qq + rr >= pw.Dp) << 31);
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, vp[qq]), rsrc,
+            (lo + (unsigned)qq * q8) | bad, 0, SMCV_NT_STORE ? 2 : 0);
+      }
     }
   };
   // stage k: W(T-1) W(T-2) R(0) | S(k-1) W(T-2-k) R(k) | S(T-2)
   auto drain_stage = [&]<int Q, int k>() __attribute__((always_inline)) {
-    if constexpr (k == 0) {
+    if constexpr (SMCV_SP_ABLATE & 1) {
+    } else if constexpr (k == 0) {
       write_block.template operator()<Q, T - 1>();
       write_block.template operator()<Q, T - 2>();
       read_chunk.template operator()<0>();
@@ -315,12 +329,16 @@ __global__ __launch_bounds__(sp::kThreads, 1) void band_sp(Args args) {
     p_kk = -(kL + kR);
     p_special = p_kk != 0 || k.js < 0;
     p_bytes = valid ? (int)0x80000000 : 0;
+    p_full = k.Dp == DMAX && k.x0 + kXT <= W;
     p_ob = static_cast<float*>(args.out) +
            (((int64_t)k.n * D + k.dp) * plane_stride + (int64_t)k.y * W + k.x0 + 32 * wave);
   };
 
   auto barrier = []() __attribute__((always_inline)) {
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if constexpr (SMCV_SP_ABLATE & 16)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    else
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   };
 
   // --------------------------------------------------------------------------- the steps
@@ -395,13 +413,17 @@ __global__ __launch_bounds__(sp::kThreads, 1) void band_sp(Args args) {
             constexpr int t = I_;
             if constexpr (t + 1 < T) rd(t + 1);
             __builtin_amdgcn_sched_barrier(0);
-            f32x16 c;
-            if constexpr (KS == 0)
-              c = mma(am[t & 1], bh, f32x16{});
-            else
-              c = mma(am[t & 1], bh, acc[t]);
-            c = mma(ah[t & 1], bmv, c);
-            acc[t] = mma(ah[t & 1], bh, c);
+            if constexpr (SMCV_SP_ABLATE & 8) {
+              asm volatile("" : : "v"(ah[t & 1]), "v"(am[t & 1]), "v"(bh), "v"(bmv));
+            } else {
+              f32x16 c;
+              if constexpr (KS == 0)
+                c = mma(am[t & 1], bh, f32x16{});
+              else
+                c = mma(am[t & 1], bh, acc[t]);
+              c = mma(ah[t & 1], bmv, c);
+              acc[t] = mma(ah[t & 1], bh, c);
+            }
             __builtin_amdgcn_sched_barrier(0);
             slot(std::integral_constant<int, t>{});
             __builtin_amdgcn_sched_barrier(0);

@@ -206,6 +206,11 @@ def inner_product_soft_argmin(left, right, max_disparity, mean=False, keep_volum
     states a second kernel merges, in a workspace allocated here); other shapes run the volume
     and the regression kernels back to back.
     """
+    if _traced():
+        if keep_volume:
+            return _ops().inner_product_soft_argmin(left, right, int(max_disparity), bool(mean))
+        return None, _ops().inner_product_soft_argmin_novolume(left, right, int(max_disparity),
+                                                               bool(mean))
     left, right, dev, code = _pair(left, right, "inner_product_soft_argmin")
     D = _disp(max_disparity, "inner_product_soft_argmin")
     n, c, h, w = left.shape
@@ -341,6 +346,8 @@ def v4_volume(featL, featR, w1, b1, w2, b2, w3, b3, w4, b4, volume_size=48):
     (N,32,H,W) fp32 x2 -> (N,D,H,W) fp32, slice i = volume11(conv3d(interweave(L[..., i:],
     R[..., :-i]))) at x >= i, 0 elsewhere, from eval-mode-folded weights
     (``model.mobile_stereo_net_v4.fold_v4_weights``)."""
+    if _traced():
+        return _ops().v4_volume(featL, featR, w1, b1, w2, b2, w3, b3, w4, b4, int(volume_size))
     left, right, dev, code = _pair(featL, featR, "v4_volume")
     if code != _lib.SM_F32:
         raise TypeError("v4_volume: float32 features only")
@@ -481,6 +488,8 @@ def warp_by_flow_map(image, flow):
     """
     if not isinstance(image, torch.Tensor) or not isinstance(flow, torch.Tensor):
         raise TypeError("warp_by_flow_map: image and flow must be tensors")
+    if _traced():
+        return _ops().warp_by_flow_map(image, flow)
     if flow.dim() != 4:
         raise ValueError(f"warp_by_flow_map: expected a 4-D flow map, got {tuple(flow.shape)}")
     n, c, h, w = flow.shape

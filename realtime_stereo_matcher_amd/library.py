@@ -176,6 +176,60 @@ def _hard_argmax(volume: torch.Tensor) -> torch.Tensor:
         return F.hard_argmax(volume)
 
 
+def _fused(left: torch.Tensor, right: torch.Tensor, max_disparity: int,
+           mean: bool) -> tuple[torch.Tensor, torch.Tensor]:
+    with _Inside():
+        return F.inner_product_soft_argmin(left, right, max_disparity, mean=mean, keep_volume=True)
+
+
+def _fused_disp_dtype(left):
+    # autocast with half features: the two-kernel path whose soft-argmin returns fp32
+    return torch.float32 if F._autocast_fp32(left) else left.dtype
+
+
+def _fused_fake(left, right, max_disparity, mean):
+    n, _, h, w = left.shape
+    return (_empty((n, max_disparity, h, w), left),
+            _empty((n, 1, h, w), left, _fused_disp_dtype(left)))
+
+
+def _fused_novolume(left: torch.Tensor, right: torch.Tensor, max_disparity: int,
+                    mean: bool) -> torch.Tensor:
+    with _Inside():
+        return F.inner_product_soft_argmin(left, right, max_disparity, mean=mean,
+                                           keep_volume=False)[1]
+
+
+def _fused_novolume_fake(left, right, max_disparity, mean):
+    n, _, h, w = left.shape
+    return _empty((n, 1, h, w), left, _fused_disp_dtype(left))
+
+
+def _warp(image: torch.Tensor, flow: torch.Tensor) -> torch.Tensor:
+    with _Inside():
+        return F.warp_by_flow_map(image, flow)
+
+
+def _warp_fake(image, flow):
+    # the output dtype rule of functional.warp_by_flow_map: fp32 under autocast (grid_sample is
+    # an autocast fp32 op), else the shared image / flow dtype
+    n, _, h, w = flow.shape
+    odt = torch.float32 if F._autocast_fp32(image, flow) else image.dtype
+    return _empty((n, image.shape[1], h, w), image, odt)
+
+
+def _v4(featL: torch.Tensor, featR: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor,
+        w2: torch.Tensor, b2: torch.Tensor, w3: torch.Tensor, b3: torch.Tensor, w4: torch.Tensor,
+        b4: torch.Tensor, volume_size: int) -> torch.Tensor:
+    with _Inside():
+        return F.v4_volume(featL, featR, w1, b1, w2, b2, w3, b3, w4, b4, volume_size)
+
+
+def _v4_fake(featL, featR, w1, b1, w2, b2, w3, b3, w4, b4, volume_size):
+    n, _, h, w = featL.shape
+    return _empty((n, volume_size, h, w), featL, torch.float32)
+
+
 inner_product_volume = _register("inner_product_volume", _inner_product, _inner_product_fake)
 correlation_volume = _register("correlation_volume", _correlation, _correlation_fake)
 groupwise_volume = _register("groupwise_volume", _groupwise, _groupwise_fake)
@@ -187,3 +241,8 @@ soft_argmin = _register("soft_argmin", _soft_argmin, _soft_argmin_fake)
 regression_presoftmax = _register("regression_presoftmax", _presoftmax, _presoftmax_fake)
 hard_argmin = _register("hard_argmin", _hard_argmin, _argext_fake)
 hard_argmax = _register("hard_argmax", _hard_argmax, _argext_fake)
+inner_product_soft_argmin = _register("inner_product_soft_argmin", _fused, _fused_fake)
+inner_product_soft_argmin_novolume = _register("inner_product_soft_argmin_novolume",
+                                               _fused_novolume, _fused_novolume_fake)
+warp_by_flow_map = _register("warp_by_flow_map", _warp, _warp_fake)
+v4_volume = _register("v4_volume", _v4, _v4_fake)
