@@ -86,7 +86,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=None,
                     help="pairs per GPU per step (weak scaling; overrides --global-batch)")
     ap.add_argument("--chunk", type=int, default=None, help="pairs per kernel launch")
-    ap.add_argument("--algo", default="auto", choices=["auto", "sp", "h2", "h2db", "f32", "mfma", "valu"],
+    ap.add_argument("--algo", default="auto", choices=["auto", "rs", "sp", "h2", "h2db", "f32", "mfma", "valu"],
                     help="cfg2 volume kernel of --pipeline separate")
     ap.add_argument("--pipeline", default="separate",
                     choices=["separate", "fused", "fused-novolume", "interweave"])
@@ -130,7 +130,8 @@ def kernel_name(cfg, pipeline, algo):
         # software-pipelined band kernel (AUTO); other shapes the double-buffered one
         sp_shape = cfg["C"] in (16, 64) and cfg["D"] > 64
         return {"valu": "dot_volume_valu", "f32": "ip_band_f32", "mfma": "ip_band_f32",
-                "h2": "band_h2", "sp": "band_sp" if sp_shape else "band_h2db"}.get(algo, "band_h2db")
+                "h2": "band_h2", "sp": "band_sp" if sp_shape else "band_h2db",
+                "rs": "band_rs" if sp_shape else "band_h2db"}.get(algo, "band_h2db")
     if pipeline == "fused" and cfg.get("D", 0) <= 192:  # volume kept, one D pass: band_h2db FUSE 1
         return "band_h2db (fused soft-argmin, volume kept)"
     if pipeline == "fused-novolume":

@@ -37,6 +37,14 @@ enum sm_status {
   SM_EUNSUPPORTED = -4 /* sm_cv_inner_product_softargmin without a volume: shape not fused */
 };
 enum sm_argext_mode { SM_ARGMIN = 0, SM_ARGMAX = 1 };
+/* sm_cv_inner_product_softargmin*: mode = 0 (sum) or 1 (mean), optionally OR'd with */
+enum sm_fused_flags {
+  SM_FUSED_DISP_F32 = 2 /* the disparity is float32 whatever the feature dtype: the reference's
+                           autocast eval, where the volume keeps the fp16 / bf16 feature dtype and
+                           F.softmax + torch.sum run in fp32 (evaluate_stereo.py:48,
+                           mobile_disp_net_c.py:208-220); fp16 / bf16 features then take the
+                           fused band kernel too */
+};
 enum sm_regress_flags {         /* bit flags */
   SM_REGRESS_SOFTMAX = 0,      /* softmax over D inside (mobile_disp_net_c.py:208-220) */
   SM_REGRESS_PRESOFTMAXED = 1, /* input already softmaxed (mobile_stereo_net_v4.py:10-14) */
@@ -63,7 +71,10 @@ enum sm_ip_algo {
   SM_IP_MFMA_SP = 10     /* software-pipelined band kernel: one workgroup per CU, two accumulator
                             sets, the previous segment's shear and stores spread over the current
                             segment's steps (fp32, aligned rows, C = 16 or 64, D in 65..192 per
-                            pass; other shapes: MFMA_H2DB) */
+                            pass; other shapes: MFMA_H2DB) */,
+  SM_IP_MFMA_RS = 11     /* role-split band kernel: per SIMD a compute wave (MFMAs, shear ring
+                            writes) and a memory wave (feature loads and staging, ring readout,
+                            volume stores); same shapes as MFMA_SP, others: MFMA_H2DB */
 };
 
 /* Library version (major*10000 + minor*100 + patch). */
@@ -90,16 +101,22 @@ int sm_cv_inner_product_ex(const void* left, const void* right, void* out, int d
 int sm_cv_correlation_mean(const void* left, const void* right, void* out, int dtype,
                            int64_t N, int64_t C, int64_t H, int64_t W, int64_t D,
                            const int64_t* l_strides, const int64_t* r_strides, void* stream);
+/* sm_cv_correlation_mean with an explicit kernel (enum sm_ip_algo; AUTO is the plain call). */
+int sm_cv_correlation_mean_ex(const void* left, const void* right, void* out, int dtype,
+                              int64_t N, int64_t C, int64_t H, int64_t W, int64_t D,
+                              const int64_t* l_strides, const int64_t* r_strides, int algo,
+                              void* stream);
 
 /* f-1: cost volume + soft-argmin regression in one pass.
  *   mode 0: TorchInnerProductCost -- cost_volume/inner_product.py:11-42; mode 1:
  *   make_correlation_volume -- model/mobile_disp_net_c.py:188-205; each followed by
  *   disparity_regression -- model/mobile_disp_net_c.py:208-220 (= the inline soft-argmin of
  *   model/mobile_stereo_net.py:144-147).
- * disparity[n,y,x] = sum_d d * softmax_d(vol[n,:,y,x]): (N, H, W) in `dtype`; the (N, D, H, W)
- * volume is written too when out_volume != NULL.  fp32 features (W >= 4) with D <= 192 take
- * the fused band kernel (the volume is never read back; with
- * out_volume == NULL it is never written).  Other shapes run the volume and the regression as
+ * disparity[n,y,x] = sum_d d * softmax_d(vol[n,:,y,x]): (N, H, W) in `dtype` (float32 with
+ * mode | SM_FUSED_DISP_F32); the (N, D, H, W) volume (in `dtype`) is written too when
+ * out_volume != NULL.  fp32 features (W >= 4) with D <= 192 take the fused band kernel, and so
+ * do fp16 / bf16 features (4-element aligned rows) with SM_FUSED_DISP_F32 (the volume is never
+ * read back; with out_volume == NULL it is never written).  Other shapes run the volume and the regression as
  * two kernels, which needs out_volume: with out_volume == NULL they return SM_EUNSUPPORTED.
  * D == 0: the disparity is 0 (an empty softmax axis). */
 int sm_cv_inner_product_softargmin(const void* left, const void* right, void* out_volume,

@@ -14,7 +14,8 @@ SM_F32, SM_F16, SM_BF16 = 0, 1, 2
 SM_OK, SM_EINVAL, SM_EDTYPE, SM_ELAUNCH, SM_EUNSUPPORTED = 0, -1, -2, -3, -4
 SM_ARGMIN, SM_ARGMAX = 0, 1
 SM_REGRESS_SOFTMAX, SM_REGRESS_PRESOFTMAXED, SM_REGRESS_OUT_F32 = 0, 1, 2
-SM_IP_AUTO, SM_IP_VALU, SM_IP_MFMA_F32, SM_IP_MFMA_H2, SM_IP_MFMA_H2DB, SM_IP_MFMA_SP = 0, 1, 2, 5, 8, 10
+SM_FUSED_DISP_F32 = 2
+SM_IP_AUTO, SM_IP_VALU, SM_IP_MFMA_F32, SM_IP_MFMA_H2, SM_IP_MFMA_H2DB, SM_IP_MFMA_SP, SM_IP_MFMA_RS = 0, 1, 2, 5, 8, 10, 11
 
 _p = ctypes.c_void_p
 _i = ctypes.c_int
@@ -28,6 +29,7 @@ SIGNATURES = {
     "sm_cv_inner_product": [_p, _p, _p, _i, _l, _l, _l, _l, _l, _lp, _lp, _p],
     "sm_cv_inner_product_ex": [_p, _p, _p, _i, _l, _l, _l, _l, _l, _lp, _lp, _i, _p],
     "sm_cv_correlation_mean": [_p, _p, _p, _i, _l, _l, _l, _l, _l, _lp, _lp, _p],
+    "sm_cv_correlation_mean_ex": [_p, _p, _p, _i, _l, _l, _l, _l, _l, _lp, _lp, _i, _p],
     "sm_cv_groupwise": [_p, _p, _p, _i, _l, _l, _l, _l, _l, _l, _lp, _lp, _p],
     "sm_cv_inner_product_softargmin": [_p, _p, _p, _p, _i, _l, _l, _l, _l, _l, _lp, _lp, _i, _p],
     "sm_cv_inner_product_softargmin_workspace_bytes": [_l, _l, _l, _l],

@@ -70,13 +70,16 @@ extern "C" int sm_cv_inner_product_ex(const void* left, const void* right, void*
     case SM_IP_AUTO:  // the two-plane fp16 band kernel; odd shapes: the exact VALU kernel
     case SM_IP_MFMA_H2:
     case SM_IP_MFMA_H2DB:
-    case SM_IP_MFMA_SP: {
+    case SM_IP_MFMA_SP:
+    case SM_IP_MFMA_RS: {
       bool handled = false;
       // AUTO: fp32 aligned rows take the double-buffered band (band_h2db), the rest band_h2;
-      // SP: the software-pipelined band (band_sp), shapes it does not take band_h2db
-      const int variant = algo == SM_IP_MFMA_SP ? 4
+      // SP / RS: the software-pipelined (band_sp) / role-split (band_rs) band, shapes they do
+      // not take band_h2db
+      const int variant = algo == SM_IP_MFMA_SP   ? 4
+                          : algo == SM_IP_MFMA_RS ? 5
                           : (algo == SM_IP_MFMA_H2DB || algo == SM_IP_AUTO) ? 2
-                                                    : 0;
+                                                                            : 0;
       int rc = band_h2_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
                              stream, &handled, variant);
       if (handled || rc != SM_OK) return rc;
@@ -99,17 +102,47 @@ extern "C" int sm_cv_inner_product(const void* left, const void* right, void* ou
                                 SM_IP_AUTO, stream);
 }
 
+extern "C" int sm_cv_correlation_mean_ex(const void* left, const void* right, void* out,
+                                         int dtype, int64_t N, int64_t C, int64_t H, int64_t W,
+                                         int64_t D, const int64_t* l_strides,
+                                         const int64_t* r_strides, int algo, void* stream) {
+  SM_ENTRY_BEGIN
+  bool handled = false;
+  int rc = SM_OK;
+  switch (algo) {
+    case SM_IP_MFMA_F32:
+      rc = band_f32_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 1,
+                          stream, &handled);
+      break;
+    case SM_IP_AUTO:
+    case SM_IP_MFMA_H2:
+    case SM_IP_MFMA_H2DB:
+    case SM_IP_MFMA_SP:
+    case SM_IP_MFMA_RS: {
+      const int variant = algo == SM_IP_MFMA_SP   ? 4
+                          : algo == SM_IP_MFMA_RS ? 5
+                          : algo == SM_IP_MFMA_H2 ? 0
+                                                  : 2;
+      rc = band_h2_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 1, stream,
+                         &handled, variant);
+      break;
+    }
+    case SM_IP_VALU:
+      break;
+    default:
+      return fail(SM_EINVAL, "unknown inner-product algo");
+  }
+  if (handled || rc != SM_OK) return rc;
+  return dot_volume_valu_entry(left, right, out, dtype, N, C, H, W, D, 1, l_strides, r_strides,
+                               1, stream);
+}
+
 extern "C" int sm_cv_correlation_mean(const void* left, const void* right, void* out, int dtype,
                                       int64_t N, int64_t C, int64_t H, int64_t W, int64_t D,
                                       const int64_t* l_strides, const int64_t* r_strides,
                                       void* stream) {
-  SM_ENTRY_BEGIN
-  bool handled = false;
-  int rc = band_h2_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 1, stream,
-                         &handled, 2);
-  if (handled || rc != SM_OK) return rc;
-  return dot_volume_valu_entry(left, right, out, dtype, N, C, H, W, D, 1, l_strides, r_strides,
-                               1, stream);
+  return sm_cv_correlation_mean_ex(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides,
+                                   SM_IP_AUTO, stream);
 }
 
 extern "C" int sm_cv_groupwise(const void* left, const void* right, float* out, int dtype,
@@ -131,12 +164,15 @@ int fused_softargmin(const void* left, const void* right, void* out_volume, void
                      int dtype, int64_t N, int64_t C, int64_t H, int64_t W, int64_t D,
                      const int64_t* l_strides, const int64_t* r_strides, int mode,
                      void* workspace, int64_t ws_bytes, void* stream) {
-  if (mode != 0 && mode != 1) return fail(SM_EINVAL, "mode must be 0 (sum) or 1 (mean)");
+  if ((mode & ~(1 | SM_FUSED_DISP_F32)) != 0)
+    return fail(SM_EINVAL, "mode must be 0 (sum) or 1 (mean), optionally | SM_FUSED_DISP_F32");
+  const bool f32disp = (mode & SM_FUSED_DISP_F32) != 0;
   if (!valid_dtype(dtype)) return fail(SM_EDTYPE, "unsupported dtype code");
   if (ws_bytes < 0) return fail(SM_EINVAL, "negative workspace size");
   if (D == 0 && N * H * W > 0) {  // softmax over an empty axis: the weighted sum is 0
     if (disparity == nullptr) return fail(SM_EINVAL, "null disparity pointer");
-    const hipError_t e = hipMemsetAsync(disparity, 0, (size_t)(N * H * W) * elem_size(dtype),
+    const hipError_t e = hipMemsetAsync(disparity, 0,
+                                        (size_t)(N * H * W) * (f32disp ? 4 : elem_size(dtype)),
                                         as_stream(stream));
     return e == hipSuccess ? SM_OK : fail(SM_ELAUNCH, hipGetErrorString(e));
   }
@@ -150,13 +186,13 @@ int fused_softargmin(const void* left, const void* right, void* out_volume, void
                 "fused cost volume + soft-argmin needs fp32 features (W >= 4) and D <= 192, or a "
                 "workspace of sm_cv_inner_product_softargmin_workspace_bytes() for D > 192; pass "
                 "a volume buffer for the two-kernel path");
-  rc = mode == 1 ? sm_cv_correlation_mean(left, right, out_volume, dtype, N, C, H, W, D,
-                                          l_strides, r_strides, stream)
-                 : sm_cv_inner_product(left, right, out_volume, dtype, N, C, H, W, D, l_strides,
-                                       r_strides, stream);
+  rc = (mode & 1) ? sm_cv_correlation_mean(left, right, out_volume, dtype, N, C, H, W, D,
+                                            l_strides, r_strides, stream)
+                   : sm_cv_inner_product(left, right, out_volume, dtype, N, C, H, W, D, l_strides,
+                                         r_strides, stream);
   if (rc != SM_OK) return rc;
-  return softargmin_entry(out_volume, disparity, dtype, N, D, H, W, SM_REGRESS_SOFTMAX, nullptr,
-                          stream);
+  return softargmin_entry(out_volume, disparity, dtype, N, D, H, W,
+                          SM_REGRESS_SOFTMAX | (f32disp ? SM_REGRESS_OUT_F32 : 0), nullptr, stream);
 }
 }  // namespace
 

@@ -335,10 +335,10 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
 
   // Fused soft-argmin straight from the accumulators (fused_softargmin, band_common.h; shared
   // with band_h2db's FUSE 1).  No ring, no LDS: the volume-free kernel never shears.
+  // (fp16 / bf16 features: exact products, no scale -- SCALE is false for them)
   auto fuse_regs = [&](const Work& k, auto scale, auto xlt) {
-    if constexpr (std::is_same<T, float>::value)
-      fused_softargmin<TMAX, MEAN, decltype(scale)::value, decltype(xlt)::value>(acc, args, k, kL, kR,
-                                                                                 wave, lr, hh);
+    fused_softargmin<TMAX, MEAN, decltype(scale)::value, decltype(xlt)::value>(acc, args, k, kL, kR,
+                                                                               wave, lr, hh);
   };
 
   // SCALE: multiply back by 2^-(kL+kR); XLT: the segment has cells x < d (R pad rows), forced
@@ -803,6 +803,7 @@ int check_dot_args(const void* left, const void* right, const void* out, int dty
 namespace h2band {
 int band_h2db_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled);
 int band_sp_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled);
+int band_rs_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled);
 int band_h2db_fused_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st,
                         bool* handled);
 }
@@ -873,13 +874,17 @@ int band_h2_entry(const void* left, const void* right, void* out, int dtype, int
   const bool mean = mode == 1;
   a.mul = 1.0f / (float)C;
   hipStream_t st = as_stream(stream);
-  // fp32 with aligned rows: variant 4 the software-pipelined kernel (band_sp; the shapes it does
-  // not take fall through to band_h2db), variant 2 the double-buffered pipeline (band_h2db);
+  // fp32 with aligned rows: variant 4 the software-pipelined kernel (band_sp), variant 5 the
+  // role-split kernel (band_rs; the shapes they do not take fall through to band_h2db), variant 2 the double-buffered pipeline (band_h2db);
   // other shapes (and variant 0) run band_h2
   if (variant != 0 && dtype == SM_F32) {
     bool done = false;
     if (variant == 4) {  // the software-pipelined kernel; shapes it does not take: band_h2db
       rc = band_sp_run(a, N, mean, al4, st, &done);
+      if (done || rc != SM_OK) return rc;
+    }
+    if (variant == 5) {  // the role-split kernel; shapes it does not take: band_h2db
+      rc = band_rs_run(a, N, mean, al4, st, &done);
       if (done || rc != SM_OK) return rc;
     }
     rc = band_h2db_run(a, N, mean, al4, st, &done);
@@ -954,7 +959,10 @@ int band_h2_fused_entry(const void* left, const void* right, void* out, float* d
   const bool multi = a.npass > 1 && out == nullptr && workspace != nullptr &&
                      ws_bytes >= band_h2_fused_workspace_bytes(N, H, W, D) &&
                      reinterpret_cast<uintptr_t>(workspace) % 8 == 0;
-  if (!vec || dtype != SM_F32 || (a.npass != 1 && !multi) || D == 0) return SM_OK;
+  // fp16 / bf16 features with fp32 disparities (SM_FUSED_DISP_F32: the reference's autocast
+  // eval) take the band kernel's half instantiations; fp32 features the fp32 ones
+  const bool f32disp = (mode & SM_FUSED_DISP_F32) != 0;
+  if (!vec || (dtype != SM_F32 && !f32disp) || (a.npass != 1 && !multi) || D == 0) return SM_OK;
   if (multi) {
     const int64_t per = (int64_t)a.npass * a.nhw;
     a.ws_s = static_cast<double*>(workspace);
@@ -965,8 +973,26 @@ int band_h2_fused_entry(const void* left, const void* right, void* out, float* d
   a.out = out;
   a.disp = disp;
   a.mul = 1.0f / (float)C;
-  const bool mean = mode == 1;
+  const bool mean = (mode & 1) != 0;
   hipStream_t st = as_stream(stream);
+  if (dtype != SM_F32) {  // exact products of the half features, one MFMA per block and step
+    auto go_half = [&](auto tag) {
+      using T = typename decltype(tag)::type;
+      return by_tmax(a.pw, [&](auto tm) {
+        constexpr int TM = decltype(tm)::value;
+        if (out != nullptr)
+          return mean ? launch<T, T, TM, true, h2band::kNDHW, 1>(a, N, st)
+                      : launch<T, T, TM, false, h2band::kNDHW, 1>(a, N, st);
+        const int rc2 = mean ? launch<T, T, TM, true, h2band::kNDHW, 2>(a, N, st)
+                             : launch<T, T, TM, false, h2band::kNDHW, 2>(a, N, st);
+        if (rc2 != SM_OK || a.ws_m == nullptr) return rc2;
+        hipLaunchKernelGGL(fused_merge_kernel, dim3((unsigned)ceil_div(a.nhw, (int64_t)256)),
+                           dim3(256), 0, st, a.ws_s, a.ws_t, a.ws_m, a.npass, a.nhw, disp);
+        return check_launch("fused_merge_kernel");
+      });
+    };
+    return dtype == SM_F16 ? go_half(std::type_identity<__half>{}) : go_half(std::type_identity<__bf16>{});
+  }
 #ifndef SMCV_NO_DB_FUSE  // (diagnostic builds: -DSMCV_NO_DB_FUSE keeps band_h2's FUSE 1 path)
   if (out != nullptr) {  // volume kept, aligned rows: the double-buffered kernel with the fold
     bool done = false;

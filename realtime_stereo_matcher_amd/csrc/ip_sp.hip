@@ -40,7 +40,9 @@
 
 #ifndef SMCV_SP_ABLATE
 #define SMCV_SP_ABLATE 0  // diagnostics only (scripts/build_variants.py): 1 no drain stages, 2 no
-#endif                    // staging, 4 feature loads from one line, 8 no MFMA, 16 no barrier
+#endif                    // staging, 4 feature loads from one line, 8 no MFMA, 16 no barrier,
+                          // 32 no volume stores, 64 no ring writes / readouts (stores kept),
+                          // 128 no feature loads
 #ifndef SMCV_SP_SETS
 #define SMCV_SP_SETS 4  // feature-load register sets (loads issued SETS - 1 steps ahead)
 #endif
@@ -128,6 +130,9 @@ __global__ __launch_bounds__(sp::kThreads, 1) void band_sp(Args args) {
   // NSETS feature-load register sets: the loads of step j land in set j % NSETS, issued
   // NSETS - 1 steps before the step that stages them
   f32x4v sv[NSETS][8];
+  if constexpr (SMCV_SP_ABLATE & 128)
+    for (int i = 0; i < NSETS; ++i)
+      for (int kk = 0; kk < 8; ++kk) sv[i][kk] = f32x4v{1.f, -1.f, 0.5f, 2.f};
   bool okp[NSETS];  // the loaded pixel group is inside the row (else: split with a zero scale)
   auto load = [&](int set, const Work& k, int ks) __attribute__((always_inline)) {
     const int px = isR ? k.js + 4 * g : k.x0 + 4 * g - G::RW;
@@ -141,7 +146,10 @@ __global__ __launch_bounds__(sp::kThreads, 1) void band_sp(Args args) {
     asm volatile("" : "+v"(csl));
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
-      gload<false>(sv[set][kk], p);  // compiler-tracked: it places the vmcnt waits itself
+      if constexpr (SMCV_SP_ABLATE & 128)
+        asm volatile("" : "+v"(sv[set][kk]));  // no load: the registers as they are
+      else
+        gload<false>(sv[set][kk], p);  // compiler-tracked: it places the vmcnt waits itself
       p += csl;
     }
   };
@@ -225,6 +233,7 @@ __global__ __launch_bounds__(sp::kThreads, 1) void band_sp(Args args) {
   // execute in order, so the later (compiler-generated) readouts see them; extra LDS operations
   // only make the compiler's own lgkmcnt waits conservative.
   auto write_block = [&]<int Q, int t>() __attribute__((always_inline)) {
+    if constexpr (SMCV_SP_ABLATE & 64) return;
     constexpr int a = T - 2 - t;
     constexpr bool wrap = ((a + 1) & 3) == 3;  // chunks a, a+1 in slots 3 and 0
     f32x16(&acc)[T] = accp.template operator()<Q>();
@@ -275,6 +284,7 @@ __global__ __launch_bounds__(sp::kThreads, 1) void band_sp(Args args) {
     }
   };
   auto read_chunk = [&]<int a>() __attribute__((always_inline)) {
+    if constexpr (SMCV_SP_ABLATE & 64) return;
     int rr = rl, cc = cl;
     asm volatile("" : "+v"(rr), "+v"(cc));
     const unsigned rb = ringw + (unsigned)(rr * 128 + 16 * cc);
@@ -283,6 +293,7 @@ __global__ __launch_bounds__(sp::kThreads, 1) void band_sp(Args args) {
       vp[qq] = lds_load4(rb + (unsigned)(((a + 1) & 3) * kSlot + qq * 1024));
   };
   auto store_chunk = [&]<int a>() __attribute__((always_inline)) {
+    if constexpr (SMCV_SP_ABLATE & 32) return;
     float* cb = p_ob + (int64_t)(32 * a) * plane_stride;
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc(cb, (short)0, p_bytes, 0x00020000);

@@ -29,7 +29,7 @@ from . import _lib
 _DTYPES = {torch.float32: _lib.SM_F32, torch.float16: _lib.SM_F16, torch.bfloat16: _lib.SM_BF16}
 _ALGOS = {"auto": _lib.SM_IP_AUTO, "valu": _lib.SM_IP_VALU, "mfma": _lib.SM_IP_MFMA_F32,
           "f32": _lib.SM_IP_MFMA_F32, "h2": _lib.SM_IP_MFMA_H2, "h2db": _lib.SM_IP_MFMA_H2DB,
-          "sp": _lib.SM_IP_MFMA_SP}
+          "sp": _lib.SM_IP_MFMA_SP, "rs": _lib.SM_IP_MFMA_RS}
 
 
 # ----------------------------------------------------------------------------------- plumbing
@@ -172,8 +172,11 @@ def inner_product_volume(left, right, max_disparity, algo="auto"):
     return _run(fn, left, right)
 
 
-def correlation_volume(l_fmap, r_fmap, max_disp):
-    """(N,C,H,W) x2 -> (N,D,H,W): mean_c L*R(x-d) for x >= d, 0 elsewhere."""
+def correlation_volume(l_fmap, r_fmap, max_disp, algo="auto"):
+    """(N,C,H,W) x2 -> (N,D,H,W): mean_c L*R(x-d) for x >= d, 0 elsewhere (``algo``: the band
+    kernel, as for inner_product_volume)."""
+    if algo not in _ALGOS:
+        raise ValueError(f"algo must be one of {sorted(_ALGOS)}")
     if _traced():
         return _ops().correlation_volume(l_fmap, r_fmap, int(max_disp))
     left, right, dev, code = _pair(l_fmap, r_fmap, "correlation_volume")
@@ -184,10 +187,10 @@ def correlation_volume(l_fmap, r_fmap, max_disp):
         out = torch.empty((n, D, h, w), dtype=left.dtype, device=dev)
         if out.numel():
             lib = _lib.load()
-            _lib.check(lib.sm_cv_correlation_mean(
+            _lib.check(lib.sm_cv_correlation_mean_ex(
                 _ptr(left), _ptr(right), _ptr(out), code, n, c, h, w, D,
-                _lib.strides_arg(left), _lib.strides_arg(right), _stream(dev)),
-                "sm_cv_correlation_mean")
+                _lib.strides_arg(left), _lib.strides_arg(right), _ALGOS[algo], _stream(dev)),
+                "sm_cv_correlation_mean_ex")
         return out
 
     return _run(fn, left, right)
@@ -215,19 +218,20 @@ def inner_product_soft_argmin(left, right, max_disparity, mean=False, keep_volum
     D = _disp(max_disparity, "inner_product_soft_argmin")
     n, c, h, w = left.shape
     mode = 1 if mean else 0
-    if _autocast_fp32(left):
-        # autocast eval with fp16 / bf16 features: the volume keeps the feature dtype (the
-        # reference assigns into zeros of left.dtype) and the soft-argmin returns fp32; the fused
-        # kernel takes fp32 features only, so this is the two-kernel path either way
-        vol = correlation_volume(left, right, D) if mean else inner_product_volume(left, right, D)
-        return (vol if keep_volume else None), soft_argmin(vol)
+    # autocast eval with fp16 / bf16 features: the volume keeps the feature dtype (the reference
+    # assigns into zeros of left.dtype) and the soft-argmin returns fp32 -- the fused kernel's
+    # fp32-disparity mode, from the fp32 accumulators of the exact products
+    f32disp = _autocast_fp32(left)
+    if f32disp:
+        mode |= _lib.SM_FUSED_DISP_F32
 
     def call(vol, disp):
         lib = _lib.load()
-        # the workspace serves only the volume-free fused kernel over several D passes, which
-        # takes fp32 features; other dtypes fall back to the two-kernel path without it
+        # the workspace serves only the volume-free fused kernel over several D passes (fp32
+        # features, or half features with fp32 disparities); the rest falls back to the
+        # two-kernel path without it
         nws = (int(lib.sm_cv_inner_product_softargmin_workspace_bytes(n, h, w, D))
-               if vol is None and code == _lib.SM_F32 else 0)
+               if vol is None and (code == _lib.SM_F32 or f32disp) else 0)
         ws = torch.empty(nws, dtype=torch.uint8, device=dev) if nws > 0 else None
         return lib.sm_cv_inner_product_softargmin_ws(
             _ptr(left), _ptr(right), None if vol is None else _ptr(vol), _ptr(disp), code,
@@ -236,7 +240,7 @@ def inner_product_soft_argmin(left, right, max_disparity, mean=False, keep_volum
 
     def fn(keep):
         vol = torch.empty((n, D, h, w), dtype=left.dtype, device=dev) if keep else None
-        disp = torch.empty((n, 1, h, w), dtype=left.dtype, device=dev)
+        disp = torch.empty((n, 1, h, w), dtype=torch.float32 if f32disp else left.dtype, device=dev)
         if disp.numel():
             rc = call(vol, disp)
             if rc == _lib.SM_EUNSUPPORTED and vol is None:

@@ -38,14 +38,12 @@ def ops():
                  8, 663552000),
         "cfg2_h2": (lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="h2"))(*feats((8, 64, 540, 960), torch.float32)),
                     8, 663552000),
-        "cfg2_b16": (lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="b16"))(*feats((8, 64, 540, 960), torch.float32)),
-                     8, 663552000),
         "cfg2_h2db": (lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="h2db"))(*feats((8, 64, 540, 960), torch.float32)),
                       8, 663552000),
         "cfg2_sp": (lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="sp"))(*feats((8, 64, 540, 960), torch.float32)),
                     8, 663552000),
-        "cfg2_h2ws": (lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="h2ws"))(*feats((8, 64, 540, 960), torch.float32)),
-                      8, 663552000),
+        "cfg2_rs": (lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="rs"))(*feats((8, 64, 540, 960), torch.float32)),
+                    8, 663552000),
         "cfg2_fused": (lambda: (lambda L, R: lambda: F.inner_product_soft_argmin(L, R, 192, keep_volume=True))(
             *feats((8, 64, 540, 960), torch.float32)), 8, 665625600),
         "cfg2_fused_nv": (lambda: (lambda L, R: lambda: F.inner_product_soft_argmin(L, R, 192, keep_volume=False))(
@@ -56,6 +54,10 @@ def ops():
                  1, 3715891200),
         "cfg4": (lambda: (lambda L, R: lambda: F.correlation_volume(L, R, 256))(*feats((4, 16, 1080, 1920), torch.float32)),
                  4, 2388787200),
+        "cfg4_rs": (lambda: (lambda L, R: lambda: F.correlation_volume(L, R, 256, algo="rs"))(*feats((4, 16, 1080, 1920), torch.float32)),
+                    4, 2388787200),
+        "cfg4_sp": (lambda: (lambda L, R: lambda: F.correlation_volume(L, R, 256, algo="sp"))(*feats((4, 16, 1080, 1920), torch.float32)),
+                    4, 2388787200),
         "cfg4_fused_nv": (lambda: (lambda L, R: lambda: F.inner_product_soft_argmin(L, R, 256, mean=True, keep_volume=False))(
             *feats((4, 16, 1080, 1920), torch.float32)), 4, 273715200),
         # f-4: 1x32x540x960 fp32 features warped by a 2-channel flow (sigma 4 px) / a disparity map

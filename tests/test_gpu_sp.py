@@ -1,6 +1,7 @@
-"""GPU parity of the software-pipelined band kernel (algo "sp", csrc/ip_sp.hip) against the CPU
-oracle, on the shapes it takes (fp32, 4-element aligned rows, C = 16 or 64, D > 64 per pass),
-including the bench's own launch shapes (cfg2: 8 pairs per launch; cfg4: 4 pairs).
+"""GPU parity of the software-pipelined band kernel (algo "sp", csrc/ip_sp.hip) and the role-split
+band kernel (algo "rs", csrc/ip_rs.hip) against the CPU oracle, on the shapes they take (fp32,
+4-element aligned rows, C = 16 or 64, D > 64 per pass), including the bench's own launch shapes
+(cfg2: 8 pairs per launch; cfg4: 4 pairs).
 
 Reference op: TorchInnerProductCost.forward (cost_volume/inner_product.py:11-42) and
 make_correlation_volume (model/mobile_disp_net_c.py:188-205).  Tolerance: 1e-4 absolute for
@@ -15,6 +16,7 @@ from oracle import stereo_oracle as O
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-4
+ALGOS = ["sp", "rs"]
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -47,20 +49,21 @@ SP_SHAPES = [(1, 64, 3, 512, 192), (2, 64, 5, 260, 100), (3, 64, 2, 132, 128), (
              (2, 16, 2, 200, 65), (1, 64, 2, 64, 192), (5, 16, 1, 900, 160)]
 
 
+@pytest.mark.parametrize("algo", ALGOS)
 @pytest.mark.parametrize("shape", SP_SHAPES, ids=[str(s) for s in SP_SHAPES])
-def test_sp_inner_product_and_correlation(shape):
+def test_sp_inner_product_and_correlation(shape, algo):
     from realtime_stereo_matcher_amd import functional as F
 
     n, c, h, w, D = shape
     l, r = _feats(hash(shape) % 997, (n, c, h, w))
-    got = host(F.inner_product_volume(dev(l), dev(r), D, algo="sp"))
+    got = host(F.inner_product_volume(dev(l), dev(r), D, algo=algo))
     np.testing.assert_allclose(got, O.inner_product(l, r, D), atol=TOL, rtol=0)
     # identical to the double-buffered kernel's volume up to fp32 summation order: both use the
     # same split; compare loosely, and exactly on integer-valued features
     li, ri = _feats(7, (n, c, h, w), "int")
-    np.testing.assert_array_equal(host(F.inner_product_volume(dev(li), dev(ri), D, algo="sp")),
+    np.testing.assert_array_equal(host(F.inner_product_volume(dev(li), dev(ri), D, algo=algo)),
                                   O.inner_product(li, ri, D))
-    corr = host(F.correlation_volume(dev(l), dev(r), D))  # AUTO (sp once it is the default)
+    corr = host(F.correlation_volume(dev(l), dev(r), D, algo=algo))
     np.testing.assert_allclose(corr, O.correlation_mean(l, r, D), atol=TOL, rtol=0)
 
 
@@ -68,20 +71,22 @@ def _cell_norm(l, r, D):
     return O.inner_product(np.abs(l), np.abs(r), D)
 
 
+@pytest.mark.parametrize("algo", ALGOS)
 @pytest.mark.parametrize("scale", [1e-15, 1e-6, 1e6, 1e15])
-def test_sp_feature_scales(scale):
+def test_sp_feature_scales(scale, algo):
     """Uniformly tiny or huge features: the first segment is recomputed with a new power-of-two
     scale (the pipeline restart), later ones carry it."""
     from realtime_stereo_matcher_amd import functional as F
 
     l, r = _feats(21, (1, 64, 3, 512))
     l, r = (l * scale).astype(np.float32), (r * scale).astype(np.float32)
-    got = host(F.inner_product_volume(dev(l), dev(r), 192, algo="sp"))
+    got = host(F.inner_product_volume(dev(l), dev(r), 192, algo=algo))
     err = np.abs(got - O.inner_product(l, r, 192))
     assert (err <= 1e-5 * _cell_norm(l, r, 192) + 1e-37).all()
 
 
-def test_sp_mixed_scales():
+@pytest.mark.parametrize("algo", ALGOS)
+def test_sp_mixed_scales(algo):
     """Scale changing from row to row and pixel to pixel: restarts and carried scales mixed
     with the drain of the previous segment (its own scale)."""
     from realtime_stereo_matcher_amd import functional as F
@@ -91,14 +96,15 @@ def test_sp_mixed_scales():
     l, r = _feats(22, (n, c, h, w))
     l = (l * 10.0 ** rng.uniform(-8, 8, (n, 1, h, 1)) * 10.0 ** rng.uniform(-2, 2, (n, 1, h, w))).astype(np.float32)
     r = (r * 10.0 ** rng.uniform(-8, 8, (n, 1, h, 1)) * 10.0 ** rng.uniform(-2, 2, (n, 1, h, w))).astype(np.float32)
-    got = host(F.inner_product_volume(dev(l), dev(r), D, algo="sp"))
+    got = host(F.inner_product_volume(dev(l), dev(r), D, algo=algo))
     err = np.abs(got - O.inner_product(l, r, D))
     bound = 1e-5 * _cell_norm(l, r, D) + 1e-30
     assert (err <= bound).all(), float((err / bound).max())
 
 
+@pytest.mark.parametrize("algo", ALGOS)
 @pytest.mark.parametrize("c", [16, 64])
-def test_sp_nonfinite(c):
+def test_sp_nonfinite(c, algo):
     """+-inf features take the exact path; NaN reaches the band (max|x| does not see it) and the
     x < d cells are still forced to 0; the drained neighbours are unaffected."""
     from realtime_stereo_matcher_amd import functional as F
@@ -111,7 +117,7 @@ def test_sp_nonfinite(c):
     l[0, 2, 3, 1] = np.nan  # NaN in L next to the x < d triangle
     r[0, 1, 3, 0] = np.nan  # NaN at R pixel 0: the pad groups of the row read it
     D = 128
-    got = host(F.inner_product_volume(dev(l), dev(r), D, algo="sp"))
+    got = host(F.inner_product_volume(dev(l), dev(r), D, algo=algo))
     want = O.inner_product(l, r, D)
     np.testing.assert_array_equal(np.isnan(got), np.isnan(want))
     np.testing.assert_array_equal(np.isposinf(got), np.isposinf(want))
@@ -120,13 +126,14 @@ def test_sp_nonfinite(c):
     np.testing.assert_allclose(got[fin], want[fin], atol=TOL, rtol=0)
 
 
-def test_sp_strided_inputs():
+@pytest.mark.parametrize("algo", ALGOS)
+def test_sp_strided_inputs(algo):
     """Channel- and batch-strided views (rows contiguous) go through the ABI strides."""
     from realtime_stereo_matcher_amd import functional as F
 
     l, r = _feats(9, (2, 128, 3, 320))
     L, R = dev(l)[:, ::2], dev(r)[:, 1::2]  # C = 64 with channel stride 2 H W
-    got = host(F.inner_product_volume(L, R, 192, algo="sp"))
+    got = host(F.inner_product_volume(L, R, 192, algo=algo))
     np.testing.assert_allclose(got, O.inner_product(l[:, ::2], r[:, 1::2], 192), atol=TOL, rtol=0)
 
 
@@ -139,7 +146,8 @@ def _check_rows(vol, ln, rn, D, rows, mean=False):
                                        err_msg=f"pair {n} row {y}")
 
 
-def test_sp_cfg2_bench_launch_shape():
+@pytest.mark.parametrize("algo", ALGOS)
+def test_sp_cfg2_bench_launch_shape(algo):
     """The bench's launch: 8 cfg2 pairs (8x64x540x960 fp32, D = 192) in ONE launch.  Rows of
     EVERY pair (first, last and the pair boundaries of the persistent schedule) against the
     oracle, the x < d triangle exactly zero, and the soft-argmin of every sampled row."""
@@ -148,7 +156,7 @@ def test_sp_cfg2_bench_launch_shape():
     g = torch.Generator(device="cuda").manual_seed(3)
     L = torch.randn(8, 64, 540, 960, device="cuda", generator=g)
     R = torch.randn(8, 64, 540, 960, device="cuda", generator=g)
-    vol = F.inner_product_volume(L, R, 192, algo="sp")
+    vol = F.inner_product_volume(L, R, 192, algo=algo)
     disp = F.soft_argmin(vol)
     torch.cuda.synchronize()
     ln, rn = host(L), host(R)
@@ -162,7 +170,8 @@ def test_sp_cfg2_bench_launch_shape():
         assert not vol[n].permute(1, 0, 2)[:, tri].any()
 
 
-def test_sp_cfg4_bench_launch_shape():
+@pytest.mark.parametrize("algo", ALGOS)
+def test_sp_cfg4_bench_launch_shape(algo):
     """The bench's cfg4 launch: 4 pairs of 16x1080x1920 fp32, correlation D = 256 (two passes of
     128 per segment) in one launch; rows of every pair against the oracle."""
     from realtime_stereo_matcher_amd import functional as F
@@ -170,6 +179,6 @@ def test_sp_cfg4_bench_launch_shape():
     g = torch.Generator(device="cuda").manual_seed(4)
     L = torch.randn(4, 16, 1080, 1920, device="cuda", generator=g)
     R = torch.randn(4, 16, 1080, 1920, device="cuda", generator=g)
-    vol = F.correlation_volume(L, R, 256)
+    vol = F.correlation_volume(L, R, 256, algo=algo)
     torch.cuda.synchronize()
     _check_rows(vol, host(L), host(R), 256, (0, 541, 1079), mean=True)

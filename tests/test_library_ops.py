@@ -136,7 +136,7 @@ def test_jit_trace_refine_and_v4_networks(v):
     with torch.no_grad():
         first = traced(*x0)
     first = first if isinstance(first, (list, tuple)) else [first]
-    assert not np.allclose(got[-1].cpu().numpy(), first[-1].cpu().numpy())  # not a constant
+    assert not np.array_equal(got[-1].cpu().numpy(), first[-1].cpu().numpy())  # not a constant
 
 
 @pytest.mark.gpu
