@@ -41,8 +41,29 @@
 #ifndef SMCV_RS_ABLATE
 #define SMCV_RS_ABLATE 0  // diagnostics only (scripts/build_variants.py): 1 no ring writes,
 #endif                    // 2 no readouts / stores, 4 no loads, 8 no MFMA, 16 no staging
+#ifndef SMCV_RS_DRAIN_C
+#define SMCV_RS_DRAIN_C 1  // 1: the compute wave reads its ring out and stores the volume (its
+#endif                     // own LDS order suffices); 0: the memory wave does (extra barrier)
 #ifndef SMCV_RS_SETS
 #define SMCV_RS_SETS 4  // feature-load register sets (loads issued SETS - 1 steps ahead)
+#endif
+
+// Diagnostic per-phase cycle counts (scripts/rs_stamps.hip only; never in libstereocv.so):
+// compute waves 0 barrier, 1 ring writes, 2 fragments + MFMA issue, 3 ring readout + store
+// issue, 4 the rest; memory waves 5 barrier, 6 load issue, 7 staging (with its load waits),
+// 8 publish + readout/stores, 9 the rest.
+#ifdef SMCV_RS_STAMPS
+namespace smcv {
+extern __device__ unsigned long long g_rs_stamps[4096][10];
+}
+#define RS_STAMP(p)                                          \
+  {                                                          \
+    const unsigned long long n_ = __builtin_amdgcn_s_memtime(); \
+    st_[p] += n_ - t_;                                       \
+    t_ = n_;                                                 \
+  }
+#else
+#define RS_STAMP(p)
 #endif
 
 namespace smcv {
@@ -100,6 +121,10 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int rw = wave & (kCW - 1);  // the 32-pixel slice (and ring) of this wave pair
+#ifdef SMCV_RS_STAMPS
+  unsigned long long st_[10] = {}, t_ = __builtin_amdgcn_s_memtime();
+#endif
+  constexpr int SB = isC ? 0 : 5;  // this role's first stamp slot
   const int lane = tid & 63;
   const int lr = lane & 31;
   const int hh = lane >> 5;
@@ -209,43 +234,60 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
   // ((128 (u - c_i) + 4 lr) mod 4096) within the chunk.
   const int u = lr - 4 * hh;
   const unsigned ring = lds_addr(smem) + (unsigned)(rw * G::RINGW);
-  auto write_block = [&]<int t>() __attribute__((always_inline)) {
+  // lane constants of the ring writes: the plain base, and the 16 folded addresses of the two
+  // straddling blocks (one per element row c_i; block 0 adds chunk T-2's offset)
+  const unsigned wb = ring + (unsigned)(512 + 128 * u + 4 * lr);
+  unsigned fold[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int ci = (i & 3) + 8 * (i >> 2);
+    fold[i] = ring + ((unsigned)(32768 + 128 * u + 4 * lr - 128 * ci) & 4095u);
+  }
+  // SPEC: the segment is scaled (kk != 0) or holds cells x < d (R pad rows, forced to 0); the
+  // plain form is one ds_write_b32 per element with an immediate offset and no vector ALU work
+  // (MEAN: one multiply)
+  auto write_block = [&]<int t, bool SPEC>() __attribute__((always_inline)) {
     if constexpr (SMCV_RS_ABLATE & 1) return;
     constexpr int a = T - 2 - t;
-    // lane bases, recomputed per block (opaque: not hoisted as invariants)
-    int uu = u, ll = lr, jl = pw.js + 32 * rw + 4 * hh;
-    asm volatile("" : "+v"(uu), "+v"(ll), "+v"(jl));
-    const unsigned wb = ring + (unsigned)(512 + 128 * uu + 4 * ll);
-    const unsigned ww = (unsigned)(32768 + 128 * uu + 4 * ll);
-    const bool special = p_special;
+    const int jl = pw.js + 32 * rw + 4 * hh;
+    const unsigned wbl = wb;  // (locals: asm operands may not name the enclosing captures)
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int ci = (i & 3) + 8 * (i >> 2);
+      const unsigned fl = fold[i];
       float val = acc[t][i];
       if constexpr (MEAN) val *= args.mul;
-      if (special) {
+      if constexpr (SPEC) {
         val = __builtin_ldexpf(val, p_kk);
         val = jl + 32 * t + ci >= 0 ? val : 0.f;  // R pad rows: cells x < d
       }
       if constexpr (a == -1 || a == T - 2) {
-        const unsigned ad = ring + ((ww - (unsigned)(128 * ci)) & 4095u);
         asm volatile("ds_write_b32 %0, %1 offset:%2"
                      :
-                     : "v"(ad), "v"(val), "n"(a == -1 ? 0 : (T - 2) * kSlot)
+                     : "v"(fl), "v"(val), "n"(a == -1 ? 0 : (T - 2) * kSlot)
                      : "memory");
       } else {
         asm volatile("ds_write_b32 %0, %1 offset:%2"
                      :
-                     : "v"(wb), "v"(val), "n"((a + 1) * kSlot - 128 * ci - 512)
+                     : "v"(wbl), "v"(val), "n"((a + 1) * kSlot - 128 * ci - 512)
                      : "memory");
       }
     }
   };
-  auto write_ring = [&]() __attribute__((always_inline)) {
-    write_block.template operator()<T - 1>();
+  // block T-1 first, then 0 .. T-2 (the folded halves are overwritten by later blocks)
+  auto write_blocks = [&]<bool SPEC>() __attribute__((always_inline)) {
+    write_block.template operator()<T - 1, SPEC>();
     [&]<int... K_>(std::integer_sequence<int, K_...>) __attribute__((always_inline)) {
-      (write_block.template operator()<K_>(), ...);
+      (write_block.template operator()<K_, SPEC>(), ...);
     }(std::make_integer_sequence<int, T - 1>{});
+  };
+  // two whole code paths on a workgroup-uniform flag (a per-element select would run the
+  // special form's ldexp / compare / select on every segment)
+  auto write_ring = [&]() __attribute__((always_inline)) {
+    if (__builtin_expect(p_special, 0))
+      write_blocks.template operator()<true>();
+    else
+      write_blocks.template operator()<false>();
   };
   const int rl = lane >> 3, cl = lane & 7;
   // chunk m of the ring: rows 8 qq + rl, pixels 4 cl .. 4 cl + 3 -> out[n, dp + 32 m + row, y,
@@ -323,12 +365,16 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
     constexpr int ld = (KS + NSETS) / NKS, lks = (KS + NSETS) % NKS;  // the loaded step
     constexpr int sset = (GS + 1) % NSETS, lset = GS % NSETS;
     const unsigned sb = bm ^ (unsigned)(G::PL0 ^ (G::PL0 + G::BUF));
+    RS_STAMP(SB + 4);
     if constexpr (isC) {
       if constexpr (KS == 0) write_ring();  // the previous segment's accumulators
+      RS_STAMP(1);
     } else {
       load(lset, wq[ld], lks);
+      RS_STAMP(6);
     }
-    if constexpr (KS == 0) barrier();  // the ring is complete (and its readers done before)
+    // the ring is complete (and its readers done before) -- when another wave reads it
+    if constexpr (KS == 0 && !SMCV_RS_DRAIN_C) barrier();
     if constexpr (isC) {
       const unsigned char* ab = smem + bm + 32 * rw * 32 + swz(lr, hh);
       const unsigned char* bb = smem + bm + (G::RW + 32 * rw) * 32 + swz(lr, hh);
@@ -355,15 +401,23 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
           acc[t] = mma(ah[t & 1], bh, c);
         }
       }
+      RS_STAMP(2);
+      if constexpr (SMCV_RS_DRAIN_C)
+        drain_range.template operator()<chunk_lo(KS, T, NKS), chunk_lo(KS + 1, T, NKS)>();
+      RS_STAMP(3);
     } else {
       if constexpr (ss == 0) mx = 0.f;  // the staged step opens its segment
       stage(sset, sb);
+      RS_STAMP(7);
       if constexpr (ss == NKS - 1) {  // the staged segment is complete: its maxima
         if (it + sd < nitems) publish_max((it + sd) & 3);
       }
-      drain_range.template operator()<chunk_lo(KS, T, NKS), chunk_lo(KS + 1, T, NKS)>();
+      if constexpr (!SMCV_RS_DRAIN_C)
+        drain_range.template operator()<chunk_lo(KS, T, NKS), chunk_lo(KS + 1, T, NKS)>();
+      RS_STAMP(8);
     }
     barrier();
+    RS_STAMP(SB);
     bm = sb;
   };
 
@@ -401,6 +455,12 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
       if constexpr (NKS == 1) publish_max(it & 3);
 #pragma unroll
       for (int k = 1; k < NSETS; ++k) load((GS0 + k) % NSETS, wq[k / NKS], k % NKS);
+      // A (re)start may land its loads in other registers than the steady-state loop, which
+      // copies them over at the join; the compiler's wait placement merges both paths, and a
+      // load pending in the restart's registers would become a wait at every segment's first
+      // step (sets 1 and 2 forced complete: measured in the asm).  Waiting here (a compiler-
+      // visible vmcnt(0); restarts are rare) leaves nothing pending on this path.
+      __builtin_amdgcn_s_waitcnt(0x0F70);
     }
     barrier();
   };
@@ -468,9 +528,14 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
   }();
   // the last segment: into the ring, then out
   if constexpr (isC) write_ring();
-  barrier();
-  if constexpr (!isC) drain_range.template operator()<0, T - 1>();
+  if constexpr (!SMCV_RS_DRAIN_C) barrier();
+  if constexpr (isC == (bool)SMCV_RS_DRAIN_C) drain_range.template operator()<0, T - 1>();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing in flight when the registers die
+#ifdef SMCV_RS_STAMPS
+  RS_STAMP(SB + 4);
+  if (lane == 0)
+    for (int p = 0; p < 10; ++p) g_rs_stamps[(blockIdx.x * 8 + wave) & 4095][p] = st_[p];
+#endif
 }
 
 template <bool MEAN, int TMAX, int NKS, int NSETS>

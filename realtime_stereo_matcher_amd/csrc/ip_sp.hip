@@ -479,6 +479,9 @@ __global__ __launch_bounds__(sp::kThreads, 1) void band_sp(Args args) {
     if constexpr (NKS == 1) publish_max(it & 3);
 #pragma unroll
     for (int k = 1; k < NSETS; ++k) load((GS0 + k) % NSETS, wq[k / NKS], k % NKS);
+    // nothing pending on this path at the loop join (see ip_rs.hip: the compiler's wait
+    // placement would otherwise carry the restart's registers into every segment's first step)
+    __builtin_amdgcn_s_waitcnt(0x0F70);
     barrier();
   };
   prologue.template operator()<0>();
