@@ -90,6 +90,9 @@ def parse():
                     help="cfg2 volume kernel of --pipeline separate")
     ap.add_argument("--pipeline", default="separate",
                     choices=["separate", "fused", "fused-novolume", "interweave"])
+    ap.add_argument("--features", default=None, choices=["f32", "f16", "bf16"],
+                    help="cfg2 / cfg4 feature dtype; f16 / bf16 run under torch.autocast as the "
+                         "reference's fp16 mode does (fp32 disparities)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
                     help="bounded CPU-baseline sample length (0 disables)")
     ap.add_argument("--no-check", action="store_true", help="skip the numerics check")
@@ -106,7 +109,8 @@ def pair_bytes(cfg, pipeline):
         return feats + cfg["G"] * H * W * D * 4
     if cfg["op"] == "concat":
         return feats + 2 * C * H * W * D * es
-    vol, disp = D * H * W * es, H * W * es
+    # disparities: fp32 under autocast (half features), else the feature dtype
+    vol, disp = D * H * W * es, H * W * max(es, 4 if cfg.get("autocast") else es)
     if pipeline == "fused":
         return feats + vol + disp
     if pipeline == "fused-novolume":
@@ -127,11 +131,11 @@ def kernel_name(cfg, pipeline, algo):
         return "band_h2 (NGHWD, bf16)"
     if cfg["op"] in ("inner_product", "correlation") and pipeline == "separate":
         # fp32 aligned rows with C = 16 or 64 and > 64 disparities per pass (cfg2, cfg4): the
-        # software-pipelined band kernel (AUTO); other shapes the double-buffered one
+        # role-split band kernel (AUTO, rs); other shapes the double-buffered one
         sp_shape = cfg["C"] in (16, 64) and cfg["D"] > 64
         return {"valu": "dot_volume_valu", "f32": "ip_band_f32", "mfma": "ip_band_f32",
-                "h2": "band_h2", "sp": "band_sp" if sp_shape else "band_h2db",
-                "rs": "band_rs" if sp_shape else "band_h2db"}.get(algo, "band_h2db")
+                "h2": "band_h2", "h2db": "band_h2db",
+                "sp": "band_sp" if sp_shape else "band_h2db"}.get(algo, "band_rs" if sp_shape else "band_h2db")
     if pipeline == "fused" and cfg.get("D", 0) <= 192:  # volume kept, one D pass: band_h2db FUSE 1
         return "band_h2db (fused soft-argmin, volume kept)"
     if pipeline == "fused-novolume":
@@ -148,6 +152,10 @@ def arithmetic(cfg, pipeline, algo):
         return "exact fp32 products on v_mfma_f32_16x16x4_f32"
     if cfg["op"] == "inner_product" and pipeline == "separate" and algo == "valu":
         return "fp32 FMA (VALU)"
+    if cfg.get("autocast"):
+        return (f"exact {cfg['dname']} products on v_mfma_f32_32x32x16_{cfg['dname']}, fp32 accumulate"
+                + ("; soft-argmin online in fp32/fp64 on the fp32 accumulators, fp32 disparities"
+                   if pipeline.startswith("fused") else "; volume rounded to the feature dtype"))
     return ARITH_SPLIT + ("; soft-argmin online in fp32/fp64" if pipeline.startswith("fused") else
                           "; soft-argmin kernel fp64 accumulation")
 
@@ -161,6 +169,12 @@ def make_step(cfg, a, L, R, ev):
     nb = L.shape[0]
 
     def dominant(l, r):
+        if cfg.get("autocast"):  # the reference's fp16 mode: the half features under autocast
+            with torch.autocast("cuda", dtype=cfg["dtype"]):
+                return dominant_(l, r)
+        return dominant_(l, r)
+
+    def dominant_(l, r):
         if cfg["op"] == "inner_product":
             if a.pipeline == "separate":
                 return F.inner_product_volume(l, r, D, algo=a.algo), None
@@ -350,9 +364,12 @@ def cpu_baseline(cfg, a, seconds):
     C, H, W, D = cfg["C"], cfg["H"], cfg["W"], cfg["D"]
     g = torch.Generator().manual_seed(0)
 
+    # the reference's CPU path computes in fp32 (autocast is a GPU mode)
+    dt = torch.float32 if cfg.get("autocast") else cfg["dtype"]
+
     def run(rows):
-        l = torch.randn(1, C, rows, W, generator=g).to(cfg["dtype"])
-        r = torch.randn(1, C, rows, W, generator=g).to(cfg["dtype"])
+        l = torch.randn(1, C, rows, W, generator=g).to(dt)
+        r = torch.randn(1, C, rows, W, generator=g).to(dt)
         t0 = time.perf_counter()
         if cfg["op"] == "inner_product":
             P.cv_plus_regression(l, r, D)
@@ -382,7 +399,8 @@ def cpu_baseline(cfg, a, seconds):
     if cfg["op"] == "concat" and a.pipeline == "interweave":
         what = "shifted interweave volume"
     return {"value": pairs / elapsed, "unit": "pairs/s", "cores": threads, "kind": "port",
-            "sample": f"{done_rows} rows of {H} ({pairs:.3f} pairs) of 1x{C}x{H}x{W} {cfg['dname']}, "
+            "sample": f"{done_rows} rows of {H} ({pairs:.3f} pairs) of 1x{C}x{H}x{W} "
+                      f"{'f32' if cfg.get('autocast') else cfg['dname']}, "
                       f"D={D}, {what}; eager torch CPU port of the reference op sequence, {threads} "
                       f"threads; host: {model}, {os.cpu_count()} logical CPUs, "
                       f"{phys or 'unknown'} physical cores",
@@ -390,13 +408,13 @@ def cpu_baseline(cfg, a, seconds):
 
 
 # ----------------------------------------------------------------------------- PMC traffic
-EVIDENCE_ROUND = "r03"
+EVIDENCE_ROUND = "r04"
 
 
 def evidence_name(a):
     suffix = {"separate": "", "fused": "_fused", "fused-novolume": "_fused_novolume",
               "interweave": "_interweave"}[a.pipeline]
-    return a.config + suffix
+    return a.config + suffix + ("" if getattr(a, "features", None) in (None, "f32") else "_" + a.features)
 
 
 def committed_traffic(a, kernel, world=1):
@@ -427,6 +445,12 @@ def committed_traffic(a, kernel, world=1):
 def main():
     a = parse()
     cfg = CONFIGS[a.config]
+    if a.features not in (None, "f32"):
+        if cfg["op"] not in ("inner_product", "correlation") or not a.pipeline.startswith("fused"):
+            raise SystemExit("--features f16 / bf16 applies to cfg2 / cfg4 with --pipeline fused*")
+        half = {"f16": torch.float16, "bf16": torch.bfloat16}[a.features]
+        cfg = dict(cfg, dtype=half, dname=a.features, autocast=True,
+                   workload=cfg["workload"] + f"; {a.features} features under torch.autocast")
     if a.pipeline in ("fused", "fused-novolume") and cfg["op"] not in ("inner_product", "correlation"):
         raise SystemExit("--pipeline fused* applies to cfg2 / cfg4 (fused volume + soft-argmin)")
     if a.pipeline == "interweave" and cfg["op"] != "concat":

@@ -66,15 +66,16 @@ enum sm_ip_algo {
   /* 7: reserved (16-pixel waves on 16x16x32 MFMA, retired in round 4: slower than MFMA_H2DB) */
   SM_IP_MFMA_H2DB = 8,   /* MFMA_H2 with double-buffered planes: the next step is staged inside
                             the current step's MFMA phase (fp32, aligned rows; else MFMA_H2; the
-                            fallback of MFMA_SP and of AUTO) */
+                            fallback of MFMA_SP, MFMA_RS and AUTO) */
   /* 9: reserved (store waves fed through an LDS queue, retired in round 4: slower) */
   SM_IP_MFMA_SP = 10     /* software-pipelined band kernel: one workgroup per CU, two accumulator
                             sets, the previous segment's shear and stores spread over the current
                             segment's steps (fp32, aligned rows, C = 16 or 64, D in 65..192 per
                             pass; other shapes: MFMA_H2DB) */,
-  SM_IP_MFMA_RS = 11     /* role-split band kernel: per SIMD a compute wave (MFMAs, shear ring
-                            writes) and a memory wave (feature loads and staging, ring readout,
-                            volume stores); same shapes as MFMA_SP, others: MFMA_H2DB */
+  SM_IP_MFMA_RS = 11     /* role-split band kernel: per SIMD a compute wave (MFMAs, shear ring,
+                            volume stores) and a memory wave (feature loads and staging); same
+                            shapes as MFMA_SP, others: MFMA_H2DB.  AUTO's choice for the shapes
+                            it takes */
 };
 
 /* Library version (major*10000 + minor*100 + patch). */

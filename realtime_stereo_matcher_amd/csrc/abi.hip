@@ -73,13 +73,14 @@ extern "C" int sm_cv_inner_product_ex(const void* left, const void* right, void*
     case SM_IP_MFMA_SP:
     case SM_IP_MFMA_RS: {
       bool handled = false;
-      // AUTO: fp32 aligned rows take the double-buffered band (band_h2db), the rest band_h2;
-      // SP / RS: the software-pipelined (band_sp) / role-split (band_rs) band, shapes they do
-      // not take band_h2db
-      const int variant = algo == SM_IP_MFMA_SP   ? 4
-                          : algo == SM_IP_MFMA_RS ? 5
-                          : (algo == SM_IP_MFMA_H2DB || algo == SM_IP_AUTO) ? 2
-                                                                            : 0;
+      // AUTO / RS: fp32 aligned rows with C = 16 or 64 and 65..192 disparities per pass take
+      // the role-split band (band_rs), other fp32 aligned rows the double-buffered one
+      // (band_h2db), the rest band_h2; SP: the software-pipelined band (band_sp), shapes it
+      // does not take band_h2db
+      const int variant = algo == SM_IP_MFMA_SP                              ? 4
+                          : (algo == SM_IP_MFMA_RS || algo == SM_IP_AUTO)    ? 5
+                          : algo == SM_IP_MFMA_H2DB                          ? 2
+                                                                             : 0;
       int rc = band_h2_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
                              stream, &handled, variant);
       if (handled || rc != SM_OK) return rc;
@@ -119,10 +120,10 @@ extern "C" int sm_cv_correlation_mean_ex(const void* left, const void* right, vo
     case SM_IP_MFMA_H2DB:
     case SM_IP_MFMA_SP:
     case SM_IP_MFMA_RS: {
-      const int variant = algo == SM_IP_MFMA_SP   ? 4
-                          : algo == SM_IP_MFMA_RS ? 5
-                          : algo == SM_IP_MFMA_H2 ? 0
-                                                  : 2;
+      const int variant = algo == SM_IP_MFMA_SP                              ? 4
+                          : (algo == SM_IP_MFMA_RS || algo == SM_IP_AUTO)    ? 5
+                          : algo == SM_IP_MFMA_H2                            ? 0
+                                                                             : 2;
       rc = band_h2_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 1, stream,
                          &handled, variant);
       break;

@@ -42,6 +42,17 @@ __device__ __forceinline__ int swz(int r, int h) {
   return ((r ^ ((r >> 2) & 3)) << 5) + ((h ^ ((r >> 4) & 1)) << 4);
 }
 
+// n / d for 32-bit n by one 64-bit high multiply: m = floor(2^64 / d) + 1 is exact for every
+// n < 2^32 (the error n e / 2^64 < 2^-32 stays below 1 / d); m = 0 marks d = 1.
+struct FastDiv {
+  unsigned long long m;
+  unsigned d;
+};
+inline FastDiv make_fastdiv(unsigned d) { return {d == 1 ? 0ull : ~0ull / d + 1, d}; }
+__device__ __forceinline__ unsigned fdiv(unsigned n, const FastDiv& f) {
+  return f.m ? (unsigned)__umul64hi((unsigned long long)n, f.m) : n;
+}
+
 struct Args {
   const void* L;
   const void* R;
@@ -57,11 +68,32 @@ struct Args {
   double* ws_t;
   float* ws_m;
   int64_t nhw;  // N H W: the workspace's per-pass stride
+  // the decode's divisors (npass, tiles, G, H) as multiplies (band_rs, set by its launcher)
+  FastDiv fd_np, fd_tiles, fd_g, fd_h;
 };
 
 struct Work {
   int n, y, g, x0, dp, Dp, js, pass;
 };
+
+// decode() with the divisions as multiplies (Args::fd_*)
+__device__ __forceinline__ Work decode_fd(unsigned w, const Args& a, int dmax) {
+  Work k;
+  const unsigned r1 = fdiv(w, a.fd_np);
+  k.pass = (int)(w - r1 * (unsigned)a.npass);
+  const unsigned r2 = fdiv(r1, a.fd_tiles);
+  const int tile = (int)(r1 - r2 * (unsigned)a.tiles);
+  const unsigned row = fdiv(r2, a.fd_g);
+  k.g = (int)(r2 - row * (unsigned)a.G);
+  const unsigned nn = fdiv(row, a.fd_h);
+  k.y = (int)(row - nn * (unsigned)a.H);
+  k.n = (int)nn;
+  k.x0 = tile * kXT;
+  k.dp = k.pass * a.pw;
+  k.Dp = min(a.pw, a.D - k.dp);
+  k.js = k.x0 - k.dp - dmax;
+  return k;
+}
 
 // work index w = (((n H + y) G + g) tiles + tile) npass + pass: consecutive items are
 // neighbouring segments of one row (and group), which share right-window columns in L2
@@ -266,6 +298,14 @@ struct Sched {
     none = gi >= scnt;  // the whole workgroup leaves together
     nitems = none ? 0 : ((scnt - gi + gsz - 1) / gsz) * np;
     rot = (gsz & 7) == 0;
+  }
+  __device__ __forceinline__ int item_fd(int i, const FastDiv& fnp) const {
+    const int si = (int)fdiv((unsigned)i, fnp);
+    const int p = i - si * npass;
+    const int j = gi + si * gsz;
+    const int b = j & ~7;
+    const int seg = sbeg + ((rot && b + 8 <= scnt) ? (b | ((j + si) & 7)) : j);
+    return seg * npass + p;
   }
   __device__ __forceinline__ int item(int i) const {
     const int si = npass == 1 ? i : i / npass;

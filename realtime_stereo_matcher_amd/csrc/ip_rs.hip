@@ -40,7 +40,8 @@
 
 #ifndef SMCV_RS_ABLATE
 #define SMCV_RS_ABLATE 0  // diagnostics only (scripts/build_variants.py): 1 no ring writes,
-#endif                    // 2 no readouts / stores, 4 no loads, 8 no MFMA, 16 no staging
+#endif                    // 2 no readouts / stores, 4 no loads, 8 no MFMA, 16 no staging,
+                          // 32 feature loads from a few L2-resident lines
 #ifndef SMCV_RS_DRAIN_C
 #define SMCV_RS_DRAIN_C 1  // 1: the compute wave reads its ring out and stores the volume (its
 #endif                     // own LDS order suffices); 0: the memory wave does (extra barrier)
@@ -116,7 +117,9 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
   const Sched sched(args.nwork, args.npass);
   if (sched.none) return;  // the whole workgroup leaves together
   const int nitems = sched.nitems;
-  auto witem = [&](int i) -> Work { return decode(sched.item(min(i, nitems - 1)), args, DMAX); };
+  auto witem = [&](int i) -> Work {
+    return decode_fd((unsigned)sched.item_fd(min(i, nitems - 1), args.fd_np), args, DMAX);
+  };
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -152,11 +155,12 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
       }
       return;
     }
-    const int pxc = min(max(px, 0), W - 4);  // pad groups: the nearest valid group
+    int pxc = min(max(px, 0), W - 4);  // pad groups: the nearest valid group
+    if constexpr (SMCV_RS_ABLATE & 32) pxc = 4 * (lane & 7);  // L2-resident lines only
     const float* p = (isR ? R + (int64_t)k.n * rs.n + (int64_t)k.y * rs.h
                           : L + (int64_t)k.n * ls.n + (int64_t)k.y * ls.h) +
-                     pxc + (int64_t)(ks * kKC + 8 * ch) * cs;
-    int64_t csl = cs;
+                     pxc + (SMCV_RS_ABLATE & 32 ? 0 : (int64_t)(ks * kKC + 8 * ch) * cs);
+    int64_t csl = SMCV_RS_ABLATE & 32 ? 0 : cs;
     asm volatile("" : "+v"(csl));
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
@@ -292,14 +296,18 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
   const int rl = lane >> 3, cl = lane & 7;
   // chunk m of the ring: rows 8 qq + rl, pixels 4 cl .. 4 cl + 3 -> out[n, dp + 32 m + row, y,
   // x0 + 32 rw + 4 cl ..]
-  auto drain_chunk = [&]<int m>() __attribute__((always_inline)) {
+  auto drain_read = [&]<int m>(f32x4v(&vp)[4]) __attribute__((always_inline)) {
     if constexpr (SMCV_RS_ABLATE & 2) return;
     int rr = rl, cc = cl;
     asm volatile("" : "+v"(rr), "+v"(cc));
     const unsigned rb = ring + (unsigned)(rr * 128 + 16 * cc);
-    f32x4v vp[4];
 #pragma unroll
     for (int qq = 0; qq < 4; ++qq) vp[qq] = lds_load4(rb + (unsigned)(m * kSlot + qq * 1024));
+  };
+  auto drain_store = [&]<int m>(const f32x4v(&vp)[4]) __attribute__((always_inline)) {
+    if constexpr (SMCV_RS_ABLATE & 2) return;
+    int rr = rl, cc = cl;
+    asm volatile("" : "+v"(rr), "+v"(cc));
     float* cb = p_ob + (int64_t)(32 * m) * plane_stride;
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc(cb, (short)0, p_bytes, 0x00020000);
@@ -326,7 +334,13 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
   };
   auto drain_range = [&]<int M0, int M1>() __attribute__((always_inline)) {
     [&]<int... K_>(std::integer_sequence<int, K_...>) __attribute__((always_inline)) {
-      (drain_chunk.template operator()<M0 + K_>(), ...);
+      (
+          [&]() __attribute__((always_inline)) {
+            f32x4v vp[4];
+            drain_read.template operator()<M0 + K_>(vp);
+            drain_store.template operator()<M0 + K_>(vp);
+          }(),
+          ...);
     }(std::make_integer_sequence<int, M1 - M0>{});
   };
   auto set_prev = [&](const Work& k, bool valid) __attribute__((always_inline)) {
@@ -375,6 +389,13 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
     }
     // the ring is complete (and its readers done before) -- when another wave reads it
     if constexpr (KS == 0 && !SMCV_RS_DRAIN_C) barrier();
+    // the compute wave's ring chunks of this step: the first (up to) two read before the
+    // matrix work, stored after it (the reads' latency hidden behind the MFMAs)
+    constexpr int c0 = chunk_lo(KS, T, NKS), c1 = chunk_lo(KS + 1, T, NKS);
+    constexpr int npre = SMCV_RS_DRAIN_C ? (c1 - c0 < 2 ? c1 - c0 : 2) : 0;
+    [[maybe_unused]] f32x4v pv[2][4];
+    if constexpr (isC && npre > 0) drain_read.template operator()<c0>(pv[0]);
+    if constexpr (isC && npre > 1) drain_read.template operator()<c0 + 1>(pv[1]);
     if constexpr (isC) {
       const unsigned char* ab = smem + bm + 32 * rw * 32 + swz(lr, hh);
       const unsigned char* bb = smem + bm + (G::RW + 32 * rw) * 32 + swz(lr, hh);
@@ -402,8 +423,9 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
         }
       }
       RS_STAMP(2);
-      if constexpr (SMCV_RS_DRAIN_C)
-        drain_range.template operator()<chunk_lo(KS, T, NKS), chunk_lo(KS + 1, T, NKS)>();
+      if constexpr (npre > 0) drain_store.template operator()<c0>(pv[0]);
+      if constexpr (npre > 1) drain_store.template operator()<c0 + 1>(pv[1]);
+      if constexpr (SMCV_RS_DRAIN_C) drain_range.template operator()<c0 + npre, c1>();
       RS_STAMP(3);
     } else {
       if constexpr (ss == 0) mx = 0.f;  // the staged step opens its segment
@@ -554,6 +576,10 @@ int launch_rs(Args a, int64_t N, hipStream_t st) {
   const int64_t nwork = (int64_t)a.tiles * a.H * N * a.G * a.npass;
   if (nwork > INT32_MAX / 64) return fail(SM_EINVAL, "band kernel: too much work for one launch");
   a.nwork = (int)nwork;
+  a.fd_np = make_fastdiv((unsigned)a.npass);
+  a.fd_tiles = make_fastdiv((unsigned)a.tiles);
+  a.fd_g = make_fastdiv((unsigned)a.G);
+  a.fd_h = make_fastdiv((unsigned)a.H);
   auto kern = band_rs<MEAN, TMAX, NKS, NSETS>;
   static std::atomic<unsigned long long> lds_done{0};
   const int dev = stream_device(st);
