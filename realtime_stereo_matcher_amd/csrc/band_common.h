@@ -317,6 +317,61 @@ struct Sched {
   }
 };
 
+// The fused pass's exact fp32 path for a segment the band cannot take (a non-finite value, a
+// scale fp32 cannot reach): each pixel's cells by fp32 FMA over the channels, folded online into
+// the soft-argmin in fp64 (band_rs; band_h2 keeps its own copy).  Several D passes
+// (args.ws_m): the pass's partial state, d global; a NaN cell or a +inf maximum is carried as
+// s = NaN, which fused_merge_kernel propagates; an all -inf pass contributes nothing.
+template <bool MEAN>
+__device__ __forceinline__ void slow_softargmin_f32(const Args& args, const Work& k, int tid,
+                                                    int nthreads) {
+  const float mul = MEAN ? args.mul : 1.0f;
+  const float* lrow = static_cast<const float*>(args.L) + (int64_t)k.n * args.ls.n +
+                      (int64_t)k.y * args.ls.h;
+  const float* rrow = static_cast<const float*>(args.R) + (int64_t)k.n * args.rs.n +
+                      (int64_t)k.y * args.rs.h;
+  for (int xx = tid; xx < kXT; xx += nthreads) {
+    const int x = k.x0 + xx;
+    if (x >= args.W) continue;
+    float m = -INFINITY;
+    double s = 0.0, t = 0.0;  // relative to m; t over the pass-local d
+    bool nan = false;
+    for (int d = 0; d < k.Dp; ++d) {
+      const int dg = k.dp + d;
+      float v = 0.f;
+      if (x >= dg) {
+        for (int c = 0; c < args.cpg; ++c)
+          v = __builtin_fmaf(lrow[(int64_t)c * args.ls.c + x], rrow[(int64_t)c * args.rs.c + x - dg], v);
+        v *= mul;
+      }
+      nan |= v != v;
+      if (v > m) {
+        const double f = m == -INFINITY ? 0.0 : (double)expf(m - v);
+        s *= f;
+        t *= f;
+        m = v;
+      }
+      if (m != INFINITY && m != -INFINITY) {
+        const double e = (double)expf(v - m);
+        s += e;
+        t += (double)d * e;
+      }
+    }
+    const size_t px = ((size_t)k.n * args.H + k.y) * args.W + x;
+    if (args.ws_m != nullptr) {
+      typedef __attribute__((address_space(1))) void gvoid;
+      const size_t o = (size_t)k.pass * ((size_t)args.nhw) + px;
+      const double sv = (nan || m == INFINITY) ? (double)NAN : s;
+      *reinterpret_cast<__attribute__((address_space(1))) double*>((gvoid*)(args.ws_s + o)) = sv;
+      *reinterpret_cast<__attribute__((address_space(1))) double*>((gvoid*)(args.ws_t + o)) =
+          t + (double)k.dp * sv;
+      store_one<float>(args.ws_m + o, m);
+    } else {
+      store_one<float>(args.disp + px, (nan || m == INFINITY || m == -INFINITY) ? NAN : (float)(t / s));
+    }
+  }
+}
+
 // Soft-argmin straight from a wave's band accumulators (the fused pass, f-1).  Lane (lr, hh)
 // holds, for pixel x0 + 32 wave + lr, the cells of local disparity dl = 32 (T-1-t) + u - c_i
 // (block t, element i, u = lr - 4 hh), and the lane pair (lr, 0), (lr, 1) holds every d of the

@@ -803,7 +803,8 @@ int check_dot_args(const void* left, const void* right, const void* out, int dty
 namespace h2band {
 int band_h2db_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled);
 int band_sp_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled);
-int band_rs_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled);
+int band_rs_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled,
+                int fuse);
 int band_h2db_fused_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st,
                         bool* handled);
 }
@@ -884,7 +885,7 @@ int band_h2_entry(const void* left, const void* right, void* out, int dtype, int
       if (done || rc != SM_OK) return rc;
     }
     if (variant == 5) {  // the role-split kernel; shapes it does not take: band_h2db
-      rc = band_rs_run(a, N, mean, al4, st, &done);
+      rc = band_rs_run(a, N, mean, al4, st, &done, 0);
       if (done || rc != SM_OK) return rc;
     }
     rc = band_h2db_run(a, N, mean, al4, st, &done);
@@ -993,6 +994,19 @@ int band_h2_fused_entry(const void* left, const void* right, void* out, float* d
     };
     return dtype == SM_F16 ? go_half(std::type_identity<__half>{}) : go_half(std::type_identity<__bf16>{});
   }
+#ifndef SMCV_NO_RS_FUSE  // (diagnostic builds: -DSMCV_NO_RS_FUSE keeps the band_h2db / band_h2 paths)
+  {  // the role-split kernel for the shapes it takes: FUSE 1 with the volume, else FUSE 2
+    bool done = false;
+    rc = band_rs_run(a, N, mean, al4, st, &done, out != nullptr ? 1 : 2);
+    if (rc != SM_OK) return rc;
+    if (done) {
+      if (out != nullptr || a.ws_m == nullptr) return SM_OK;
+      hipLaunchKernelGGL(fused_merge_kernel, dim3((unsigned)ceil_div(a.nhw, (int64_t)256)), dim3(256), 0,
+                         st, a.ws_s, a.ws_t, a.ws_m, a.npass, a.nhw, disp);
+      return check_launch("fused_merge_kernel");
+    }
+  }
+#endif
 #ifndef SMCV_NO_DB_FUSE  // (diagnostic builds: -DSMCV_NO_DB_FUSE keeps band_h2's FUSE 1 path)
   if (out != nullptr) {  // volume kept, aligned rows: the double-buffered kernel with the fold
     bool done = false;

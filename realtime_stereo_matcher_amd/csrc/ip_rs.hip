@@ -76,7 +76,7 @@ constexpr int kThreads = 2 * 64 * kCW;
 constexpr int kKC = 16;                // channels per step (one 32x32x16 k-step)
 constexpr int kSlot = 32 * 32 * 4;     // one ring chunk: 32 d x 32 x fp32
 
-template <int TMAX>
+template <int TMAX, int FUSE = 0>
 struct Geo {
   static constexpr int DMAX = 32 * (TMAX - 1);
   static constexpr int RW = kXT + DMAX;    // right-window rows
@@ -85,7 +85,8 @@ struct Geo {
   static constexpr int BUF = 2 * PLANE;    // h + m planes of one step
   static constexpr int GROUPS = ROWS / 4;
   static constexpr int ITEMS = 2 * GROUPS;
-  static constexpr int RINGW = (TMAX - 1) * kSlot;  // one compute wave's ring
+  // one compute wave's ring (the volume-free fused pass has none)
+  static constexpr int RINGW = FUSE == 2 ? 0 : (TMAX - 1) * kSlot;
   static constexpr int PL0 = kCW * RINGW;           // plane buffers after the rings
   static constexpr int MAXW = PL0 + 2 * BUF;        // 4 maxima sets x (max|L|, max|R|)
   static constexpr size_t SHM = (size_t)MAXW + 64;
@@ -101,10 +102,11 @@ constexpr int chunk_lo(int ks, int T, int NKS) { return (ks * (T - 1) + NKS - 1)
 // checks, restarts and barriers, all decided on workgroup-uniform data); what each does between
 // the barriers is selected at compile time, so neither role's registers (the accumulators, the
 // load sets) are live in the other's code.
-template <bool CW, bool MEAN, int TMAX, int NKS, int NSETS>
+template <bool CW, bool MEAN, int TMAX, int NKS, int NSETS, int FUSE>
 __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
   using namespace roles;
-  using G = roles::Geo<TMAX>;
+  using G = roles::Geo<TMAX, FUSE>;
+  constexpr bool VOL = FUSE != 2;  // the volume is written (FUSE 0, 1)
   constexpr int T = TMAX;
   constexpr int DMAX = G::DMAX;
   static_assert(T >= 3, "blocks 0 and T-1 are distinct and fold into distinct chunks");
@@ -288,16 +290,38 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
   // two whole code paths on a workgroup-uniform flag (a per-element select would run the
   // special form's ldexp / compare / select on every segment)
   auto write_ring = [&]() __attribute__((always_inline)) {
-    if (__builtin_expect(p_special, 0))
-      write_blocks.template operator()<true>();
-    else
-      write_blocks.template operator()<false>();
+    if constexpr (VOL) {
+      if (__builtin_expect(p_special, 0))
+        write_blocks.template operator()<true>();
+      else
+        write_blocks.template operator()<false>();
+    }
+  };
+  // FUSE: the previous segment's soft-argmin straight from the accumulators (f-1, band_common.h)
+  // before the next segment's first MFMAs overwrite them; nothing for an invalid segment
+  auto fuse_regs = [&]() __attribute__((always_inline)) {
+    if constexpr (FUSE != 0) {
+      if (p_bytes == 0) return;
+      auto go = [&](auto scale, auto xlt) __attribute__((always_inline)) {
+        fused_softargmin<T, MEAN, decltype(scale)::value, decltype(xlt)::value>(
+            acc, args, pw, -p_kk, 0, rw, lr, hh);
+      };
+      const bool sc = p_kk != 0, xl = pw.js < 0;
+      if (!sc && !xl)
+        go(std::false_type{}, std::false_type{});
+      else if (sc && !xl)
+        go(std::true_type{}, std::false_type{});
+      else if (!sc)
+        go(std::false_type{}, std::true_type{});
+      else
+        go(std::true_type{}, std::true_type{});
+    }
   };
   const int rl = lane >> 3, cl = lane & 7;
   // chunk m of the ring: rows 8 qq + rl, pixels 4 cl .. 4 cl + 3 -> out[n, dp + 32 m + row, y,
   // x0 + 32 rw + 4 cl ..]
   auto drain_read = [&]<int m>(f32x4v(&vp)[4]) __attribute__((always_inline)) {
-    if constexpr (SMCV_RS_ABLATE & 2) return;
+    if constexpr ((SMCV_RS_ABLATE & 2) || !VOL) return;
     int rr = rl, cc = cl;
     asm volatile("" : "+v"(rr), "+v"(cc));
     const unsigned rb = ring + (unsigned)(rr * 128 + 16 * cc);
@@ -305,7 +329,7 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
     for (int qq = 0; qq < 4; ++qq) vp[qq] = lds_load4(rb + (unsigned)(m * kSlot + qq * 1024));
   };
   auto drain_store = [&]<int m>(const f32x4v(&vp)[4]) __attribute__((always_inline)) {
-    if constexpr (SMCV_RS_ABLATE & 2) return;
+    if constexpr ((SMCV_RS_ABLATE & 2) || !VOL) return;
     int rr = rl, cc = cl;
     asm volatile("" : "+v"(rr), "+v"(cc));
     float* cb = p_ob + (int64_t)(32 * m) * plane_stride;
@@ -381,7 +405,10 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
     const unsigned sb = bm ^ (unsigned)(G::PL0 ^ (G::PL0 + G::BUF));
     RS_STAMP(SB + 4);
     if constexpr (isC) {
-      if constexpr (KS == 0) write_ring();  // the previous segment's accumulators
+      if constexpr (KS == 0) {  // the previous segment's accumulators
+        write_ring();
+        fuse_regs();
+      }
       RS_STAMP(1);
     } else {
       load(lset, wq[ld], lks);
@@ -392,7 +419,7 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
     // the compute wave's ring chunks of this step: the first (up to) two read before the
     // matrix work, stored after it (the reads' latency hidden behind the MFMAs)
     constexpr int c0 = chunk_lo(KS, T, NKS), c1 = chunk_lo(KS + 1, T, NKS);
-    constexpr int npre = SMCV_RS_DRAIN_C ? (c1 - c0 < 2 ? c1 - c0 : 2) : 0;
+    constexpr int npre = SMCV_RS_DRAIN_C && VOL ? (c1 - c0 < 2 ? c1 - c0 : 2) : 0;
     [[maybe_unused]] f32x4v pv[2][4];
     if constexpr (isC && npre > 0) drain_read.template operator()<c0>(pv[0]);
     if constexpr (isC && npre > 1) drain_read.template operator()<c0 + 1>(pv[1]);
@@ -445,6 +472,8 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
 
   // exact fp32 FMA path for a segment holding a non-finite value or out of the scale range
   auto slow_segment = [&](const Work& k) __attribute__((always_inline)) {
+    if constexpr (FUSE != 0) slow_softargmin_f32<MEAN>(args, k, tid, kThreads);
+    if constexpr (!VOL) return;
     const float mul = MEAN ? args.mul : 1.0f;
     float* out = static_cast<float*>(args.out);
     const float* lrow = L + (int64_t)k.n * ls.n + (int64_t)k.y * ls.h;
@@ -549,7 +578,10 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
     }
   }();
   // the last segment: into the ring, then out
-  if constexpr (isC) write_ring();
+  if constexpr (isC) {
+    write_ring();
+    fuse_regs();
+  }
   if constexpr (!SMCV_RS_DRAIN_C) barrier();
   if constexpr (isC == (bool)SMCV_RS_DRAIN_C) drain_range.template operator()<0, T - 1>();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing in flight when the registers die
@@ -560,18 +592,20 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
 #endif
 }
 
-template <bool MEAN, int TMAX, int NKS, int NSETS>
+// FUSE 0: the volume; 1: the volume and its soft-argmin; 2: the soft-argmin only (no ring, no
+// volume stores)
+template <bool MEAN, int TMAX, int NKS, int NSETS, int FUSE>
 __global__ __launch_bounds__(roles::kThreads, 1) void band_rs(Args args) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) < roles::kCW)
-    rs_role<true, MEAN, TMAX, NKS, NSETS>(args, smem);
+    rs_role<true, MEAN, TMAX, NKS, NSETS, FUSE>(args, smem);
   else
-    rs_role<false, MEAN, TMAX, NKS, NSETS>(args, smem);
+    rs_role<false, MEAN, TMAX, NKS, NSETS, FUSE>(args, smem);
 }
 
-template <bool MEAN, int TMAX, int NKS, int NSETS>
+template <bool MEAN, int TMAX, int NKS, int NSETS, int FUSE>
 int launch_rs(Args a, int64_t N, hipStream_t st) {
-  using G = roles::Geo<TMAX>;
+  using G = roles::Geo<TMAX, FUSE>;
   a.tiles = (int)ceil_div(a.W, kXT);
   const int64_t nwork = (int64_t)a.tiles * a.H * N * a.G * a.npass;
   if (nwork > INT32_MAX / 64) return fail(SM_EINVAL, "band kernel: too much work for one launch");
@@ -580,7 +614,7 @@ int launch_rs(Args a, int64_t N, hipStream_t st) {
   a.fd_tiles = make_fastdiv((unsigned)a.tiles);
   a.fd_g = make_fastdiv((unsigned)a.G);
   a.fd_h = make_fastdiv((unsigned)a.H);
-  auto kern = band_rs<MEAN, TMAX, NKS, NSETS>;
+  auto kern = band_rs<MEAN, TMAX, NKS, NSETS, FUSE>;
   static std::atomic<unsigned long long> lds_done{0};
   const int dev = stream_device(st);
   if (int rc = ensure_lds_limit(reinterpret_cast<const void*>(kern), (int)G::SHM, dev, lds_done))
@@ -596,19 +630,31 @@ int launch_rs(Args a, int64_t N, hipStream_t st) {
 // channels with NKS in {1, 4} (other channel counts: band_h2db), a pass width of more than 64
 // disparities, and 32 disparity planes spanning < 2 GB (the store offsets).
 int band_rs_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st,
-                bool* handled) {
+                bool* handled, int fuse) {
   *handled = false;
   const int nks = a.cpg / 16;
   if (!aligned4 || a.G != 1 || a.W < 4 || a.cpg % 16 != 0 || (nks != 1 && nks != 4) ||
       a.pw <= 64 || a.pw > 192 || (int64_t)a.H * a.W * 4 * 32 >= ((int64_t)1 << 31))
     return SM_OK;
+  // the mean with the volume kept, one channel step, D > 128: its compute wave would spill
+  if (fuse == 1 && mean && nks == 1 && a.pw > 128) return SM_OK;
   *handled = true;
   auto go = [&](auto tm, auto nk) {
     constexpr int TM = decltype(tm)::value, NK = decltype(nk)::value;
     // one channel step per segment: two load sets (four unroll the body over four segments,
     // whose work-item state spills)
     constexpr int NS = NK == 1 ? 2 : SMCV_RS_SETS;
-    return mean ? launch_rs<true, TM, NK, NS>(a, N, st) : launch_rs<false, TM, NK, NS>(a, N, st);
+    auto f = [&](auto fc) {
+      constexpr int FU = decltype(fc)::value;
+      if constexpr (FU == 1 && NK == 1 && TM == 7)  // (excluded above for the mean)
+        return launch_rs<false, TM, NK, NS, FU>(a, N, st);
+      else
+        return mean ? launch_rs<true, TM, NK, NS, FU>(a, N, st)
+                    : launch_rs<false, TM, NK, NS, FU>(a, N, st);
+    };
+    return fuse == 2   ? f(std::integral_constant<int, 2>{})
+           : fuse == 1 ? f(std::integral_constant<int, 1>{})
+                       : f(std::integral_constant<int, 0>{});
   };
   using I1 = std::integral_constant<int, 1>;
   using I4 = std::integral_constant<int, 4>;

@@ -16,9 +16,14 @@
 // splits into a left part PL(y,x) and a right part PR(y,x-i) that do NOT depend on i: the
 // "tables" kernel computes them once per pixel (fp32 FMA), plus the single-column pieces that
 // the crop removes (dx = -1 of L at x = i, dx = +1 of R at x = W - 1).  Layers 2 and 3 (92 k of
-// the ~110 k flops per cell) run on v_mfma_f32_32x32x16_bf16 / 16x16x32_bf16 with every fp32
-// operand split into bf16 hi + lo and three products (hh + hl + lh; |error| <= ~2^-16 relative per
-// product, fp32 accumulation).
+// the ~110 k flops per cell) run on v_mfma_f32_32x32x16_f16 / 16x16x32_f16 with every fp32
+// operand scaled by a per-layer power of two and split into fp16 hi + lo (round to nearest) and
+// three products (hh + hl + lh: exact in fp32; the dropped lo*lo' and the lo roundings leave
+// ~3 * 2^-22 relative per product; fp32 accumulation).  The scales come from bounds computed on
+// the device before the main kernel, so the scaled values stay below 2^15 (no fp16 overflow):
+// max|W2|, max|W3| directly; |a1| <= max|b1| + max|PL| + max|PR| (v4_tables records the table
+// maxima); |a2| <= max|b2| + max_o2 sum|W2[o2]| * bound(a1).  Values far below their layer's
+// bound lose only absolute precision (the fp16 subnormal step, ~2^-39 of the bound).
 //
 // Main kernel.  A workgroup owns (n, i, a 30-pixel column strip, a band of rows) and streams down
 // the rows with three-row LDS rings of a1 (34 px halo, 8 x 16 channels) and a2 (34 px, 64
@@ -34,8 +39,8 @@
 namespace smcv {
 namespace v4vol {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
@@ -47,9 +52,9 @@ constexpr int kA1 = 34;      // a1 ring pixels: 32 computed (x0-2 .. x0+29) + 2 
 constexpr int kThreads = 512;
 
 // LDS layout (bytes)
-constexpr int kA1Slot = 8 * kA1 * 16 * 2;      // one row: [b 8][p 34][16 ch] bf16
+constexpr int kA1Slot = 8 * kA1 * 16 * 2;      // one row: [b 8][p 34][16 ch] fp16
 constexpr int kA1Plane = 3 * kA1Slot;          // three rows
-constexpr int kA2Slot = kA2 * 64 * 2;          // one row: [p 34][64 ch] bf16
+constexpr int kA2Slot = kA2 * 64 * 2;          // one row: [p 34][64 ch] fp16
 constexpr int kA2Plane = 3 * kA2Slot;
 constexpr int kOffA1 = 0;                                  // hi plane, then lo plane
 constexpr int kOffA2 = kOffA1 + 2 * kA1Plane;
@@ -62,10 +67,18 @@ static_assert(kShm <= 160 * 1024, "one workgroup per CU");
 __device__ __forceinline__ int ks_begin(int g) { return g == 0 ? 0 : g == 1 ? 5 : g == 2 ? 10 : 14; }
 __device__ __forceinline__ int ks_end(int g) { return g == 0 ? 5 : g == 1 ? 10 : g == 2 ? 14 : 18; }
 
+// the scale block in the workspace (after the packed weights): the table maxima (as the bits of
+// non-negative floats, atomically max'ed by v4_tables) and the four exponents v4_pack derives
+struct Scales {
+  unsigned max_tl, max_tr;  // max |PL|, max |PR| over the four table variants
+  int k_a1, k_w2, k_a2, k_w3;
+};
+
 struct Args {
   const float* T;        // tables [n][y][x][4][128]: PL, PL without dx=-1, PR, PR without dx=+1
-  const bf16x8* P2;      // layer-2 B fragments [kd 4][tap 9][lane 64] hi, then the same lo
-  const bf16x8* P3;      // layer-3 B fragments [step 18][lane 64] hi, then lo
+  const f16x8* P2;       // layer-2 B fragments [kd 4][tap 9][lane 64] hi, then the same lo
+  const f16x8* P3;       // layer-3 B fragments [step 18][lane 64] hi, then lo
+  const Scales* S;
   const float* b1;       // (16)
   const float* b2;       // (32)
   const float* b3;       // (16)
@@ -82,13 +95,25 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-__device__ __forceinline__ void split8(const float (&v)[8], bf16x8& hi, bf16x8& lo) {
+// x 2^k -> fp16 hi = rn16(x 2^k), lo = rn16(x 2^k - hi) (the scaled value is below 2^15)
+__device__ __forceinline__ void split16(float x, int k, _Float16& hi, _Float16& lo) {
+  const float v = __builtin_ldexpf(x, k);
+  hi = (_Float16)v;
+  lo = (_Float16)(v - (float)hi);
+}
+__device__ __forceinline__ void split8(const float (&v)[8], int k, f16x8& hi, f16x8& lo) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const __bf16 h = (__bf16)v[j];
+    _Float16 h, l;
+    split16(v[j], k, h, l);
     hi[j] = h;
-    lo[j] = (__bf16)(v[j] - (float)h);
+    lo[j] = l;
   }
+}
+// exponent k with b 2^k <= 2^15 (b > 0 finite), 0 for b == 0, clamped to fp32's reach
+__device__ __forceinline__ int scale_exp(float b) {
+  if (!(b > 0.f) || !(b < 3.4e38f)) return 0;
+  return min(100, max(-100, 15 - __builtin_amdgcn_frexp_expf(b)));
 }
 
 // ------------------------------------------------------------------------------ tables
@@ -99,13 +124,18 @@ __device__ __forceinline__ void split8(const float (&v)[8], bf16x8& hi, bf16x8& 
 __global__ __launch_bounds__(256) void v4_tables(const float* __restrict__ L,
                                                  const float* __restrict__ R, Strides4 ls,
                                                  Strides4 rs, const float* __restrict__ w1,
-                                                 float* __restrict__ T, int N, int H, int W) {
+                                                 float* __restrict__ T, Scales* __restrict__ S,
+                                                 int N, int H, int W) {
   __shared__ float ws[16 * 8 * 9];
   for (int e = threadIdx.x; e < 16 * 8 * 9; e += 256) ws[e] = w1[e];
   __syncthreads();
-  const int64_t px = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  // (no early return: every lane reaches the maxima's wave reduction; a lane past the end
+  // computes pixel 0 again and stores nothing)
+  const int64_t pxl = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool live = pxl < (int64_t)N * H * W;
+  const int64_t px = live ? pxl : 0;
   const int b = blockIdx.y;
-  if (px >= (int64_t)N * H * W) return;
+  float ml = 0.f, mr = 0.f;  // this thread's table maxima (the a1 scale's bound)
   const int x = (int)(px % W);
   const int y = (int)((px / W) % H);
   const int n = (int)(px / ((int64_t)W * H));
@@ -138,46 +168,104 @@ __global__ __launch_bounds__(256) void v4_tables(const float* __restrict__ L,
         if (t % 3 == 2) prp += r;
       }
     }
-    o[o1] = pl;
-    o[kCh + o1] = pl - plm;
-    o[2 * kCh + o1] = pr;
-    o[3 * kCh + o1] = pr - prp;
+    if (live) {
+      o[o1] = pl;
+      o[kCh + o1] = pl - plm;
+      o[2 * kCh + o1] = pr;
+      o[3 * kCh + o1] = pr - prp;
+    }
+    ml = fmaxf(ml, fmaxf(fabsf(pl), fabsf(pl - plm)));
+    mr = fmaxf(mr, fmaxf(fabsf(pr), fabsf(pr - prp)));
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    ml = fmaxf(ml, __shfl_xor(ml, o));
+    mr = fmaxf(mr, __shfl_xor(mr, o));
+  }
+  // non-negative floats order as their bits; NaN (bits above +inf) makes the bound non-finite,
+  // and v4_pack then leaves the scale at 2^0
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(&S->max_tl, __float_as_uint(ml));
+    atomicMax(&S->max_tr, __float_as_uint(mr));
   }
 }
 
 // ------------------------------------------------------------------------------ weight packing
-// The MFMA B fragments, split into bf16 hi / lo.  Layer 2 (32x32x16): lane l holds
+// One workgroup: the scale exponents (from the weights, the biases and the table maxima), then
+// the MFMA B fragments, scaled and split into fp16 hi / lo.  Layer 2 (32x32x16): lane l holds
 // B[k = 8 (l>>5) + j][col l&31] = W2[o2 = l&31][o1 = 8 (l>>5) + j][kd][dy][dx].  Layer 3
 // (16x16x32): step s = 2 tap + half, lane l holds B[k = 8 (l>>4) + j][col l&15] =
 // W3[o3 = l&15][o2 = k][kd = half][dy][dx].
-__global__ __launch_bounds__(256) void v4_pack(const float* __restrict__ w2,
-                                               const float* __restrict__ w3,
-                                               __bf16* __restrict__ P2, __bf16* __restrict__ P3) {
-  constexpr int n2 = 4 * 9 * 64 * 8, n3 = 18 * 64 * 8;
-  for (int e = threadIdx.x + blockIdx.x * 256; e < n2 + n3; e += 256 * gridDim.x) {
-    float v;
-    __bf16* hp;
-    int off, total;
+__global__ __launch_bounds__(1024) void v4_pack(const float* __restrict__ w2,
+                                                const float* __restrict__ w3,
+                                                const float* __restrict__ b1,
+                                                const float* __restrict__ b2,
+                                                _Float16* __restrict__ P2, _Float16* __restrict__ P3,
+                                                Scales* __restrict__ S) {
+  constexpr int n2 = 4 * 9 * 64 * 8, n3 = 18 * 64 * 8;  // = the sizes of W2, W3
+  __shared__ float red[4][32];
+  __shared__ float rows[32];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float m2 = 0.f, m3 = 0.f, mb1 = 0.f, mb2 = 0.f;
+  for (int e = tid; e < n2; e += 1024) m2 = fmaxf(m2, fabsf(w2[e]));
+  for (int e = tid; e < n3; e += 1024) m3 = fmaxf(m3, fabsf(w3[e]));
+  if (tid < 16) mb1 = fabsf(b1[tid]);
+  if (tid < 32) mb2 = fabsf(b2[tid]);
+  // row sums of |W2| (576 terms per output channel o2): wave o2 & 15, two rows per wave
+  if (tid < 32) rows[tid] = 0.f;
+  __syncthreads();
+  for (int o2 = wave; o2 < 32; o2 += 16) {
+    float r = 0.f;
+    for (int e = lane; e < 576; e += 64) r += fabsf(w2[o2 * 576 + e]);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) r += __shfl_xor(r, o);
+    if (lane == 0) rows[o2] = r;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    m2 = fmaxf(m2, __shfl_xor(m2, o));
+    m3 = fmaxf(m3, __shfl_xor(m3, o));
+    mb1 = fmaxf(mb1, __shfl_xor(mb1, o));
+    mb2 = fmaxf(mb2, __shfl_xor(mb2, o));
+  }
+  if (lane == 0) {
+    red[0][wave] = m2;
+    red[1][wave] = m3;
+    red[2][wave] = mb1;
+    red[3][wave] = mb2;
+  }
+  __syncthreads();
+  __shared__ int ks[4];
+  if (tid == 0) {
+    float v[4] = {0.f, 0.f, 0.f, 0.f}, rmax = 0.f;
+    for (int w = 0; w < 16; ++w)
+      for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], red[q][w]);
+    for (int o2 = 0; o2 < 32; ++o2) rmax = fmaxf(rmax, rows[o2]);
+    const float ba1 = v[2] + __uint_as_float(S->max_tl) + __uint_as_float(S->max_tr);
+    const float ba2 = v[3] + rmax * ba1;
+    ks[0] = scale_exp(ba1);
+    ks[1] = scale_exp(v[0]);
+    ks[2] = scale_exp(ba2);
+    ks[3] = scale_exp(v[1]);
+    S->k_a1 = ks[0];
+    S->k_w2 = ks[1];
+    S->k_a2 = ks[2];
+    S->k_w3 = ks[3];
+  }
+  __syncthreads();
+  const int kw2 = ks[1], kw3 = ks[3];
+  for (int e = tid; e < n2 + n3; e += 1024) {
     if (e < n2) {
-      const int j = e & 7, lane = (e >> 3) & 63, tap = (e >> 9) % 9, kd = (e >> 9) / 9;
-      const int o2 = lane & 31, o1 = 8 * (lane >> 5) + j;
-      v = w2[(((o2 * 16 + o1) * 4 + kd) * 3 + tap / 3) * 3 + tap % 3];
-      hp = P2;
-      off = e;
-      total = n2;
+      const int j = e & 7, ln = (e >> 3) & 63, tap = (e >> 9) % 9, kd = (e >> 9) / 9;
+      const int o2 = ln & 31, o1 = 8 * (ln >> 5) + j;
+      split16(w2[(((o2 * 16 + o1) * 4 + kd) * 3 + tap / 3) * 3 + tap % 3], kw2, P2[e], P2[n2 + e]);
     } else {
       const int f = e - n2;
-      const int j = f & 7, lane = (f >> 3) & 63, s = f >> 9;
-      const int tap = s >> 1, half = s & 1;
-      const int o3 = lane & 15, o2 = 8 * (lane >> 4) + j;
-      v = w3[(((o3 * 32 + o2) * 2 + half) * 3 + tap / 3) * 3 + tap % 3];
-      hp = P3;
-      off = f;
-      total = n3;
+      const int j = f & 7, ln = (f >> 3) & 63, st = f >> 9;
+      const int tap = st >> 1, half = st & 1;
+      const int o3 = ln & 15, o2 = 8 * (ln >> 4) + j;
+      split16(w3[(((o3 * 32 + o2) * 2 + half) * 3 + tap / 3) * 3 + tap % 3], kw3, P3[f], P3[n3 + f]);
     }
-    const __bf16 h = (__bf16)v;
-    hp[off] = h;
-    hp[total + off] = (__bf16)(v - (float)h);
   }
 }
 
@@ -205,8 +293,10 @@ __global__ __launch_bounds__(kThreads, 1) void v4_main(Args a) {
     return;
   }
 
-  // ---- resident weights
-  bf16x8 w2h[9], w2l[9];
+  // ---- the layers' scale exponents (v4_pack) and the resident weights
+  const int ka1 = a.S->k_a1, ka2 = a.S->k_a2;
+  const int kout2 = -(ka1 + a.S->k_w2), kout3 = -(ka2 + a.S->k_w3);
+  f16x8 w2h[9], w2l[9];
   {
     const int kd = wave & 3;
 #pragma unroll
@@ -217,7 +307,7 @@ __global__ __launch_bounds__(kThreads, 1) void v4_main(Args a) {
   }
   const int mb = wave & 1, kg = wave >> 1;  // layer 3: 16-pixel half, K group
   const int s0 = ks_begin(kg), s1 = ks_end(kg);
-  bf16x8 w3h[5], w3l[5];
+  f16x8 w3h[5], w3l[5];
 #pragma unroll
   for (int q = 0; q < 5; ++q) {
     const int s = min(s0 + q, 17);
@@ -265,17 +355,17 @@ __global__ __launch_bounds__(kThreads, 1) void v4_main(Args a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j)
       v[j] = ok ? fmaxf(bias1[j] + (pf.pl[j >> 2][j & 3] + pf.pr[j >> 2][j & 3]), 0.f) : 0.f;
-    bf16x8 h, l;
-    split8(v, h, l);
+    f16x8 h, l;
+    split8(v, ka1, h, l);
     const int off = slot * kA1Slot + ((wave * kA1 + pp) * 16 + hh * 8) * 2;
-    *reinterpret_cast<bf16x8*>(a1h + off) = h;
-    *reinterpret_cast<bf16x8*>(a1l + off) = l;
+    *reinterpret_cast<f16x8*>(a1h + off) = h;
+    *reinterpret_cast<f16x8*>(a1l + off) = l;
   };
   // the a1 ring's two pad pixels stay zero
   for (int e = tid; e < 2 * 3 * 8 * 2 * 2; e += kThreads) {
     const int pl = e & 1, pad = (e >> 1) & 1, hv = (e >> 2) & 1, b = (e >> 3) % 8, sl = (e >> 3) / 8;
-    const bf16x8 z = {};
-    *reinterpret_cast<bf16x8*>((pl ? a1l : a1h) + sl * kA1Slot + ((b * kA1 + 32 + pad) * 16 + hv * 8) * 2) = z;
+    const f16x8 z = {};
+    *reinterpret_cast<f16x8*>((pl ? a1l : a1h) + sl * kA1Slot + ((b * kA1 + 32 + pad) * 16 + hv * 8) * 2) = z;
   }
 
   // one output-row step; the a1 table rows are prefetched two steps ahead, alternating between
@@ -295,17 +385,17 @@ __global__ __launch_bounds__(kThreads, 1) void v4_main(Args a) {
         const int slot = ((q + dy - 1) % 3 + 3) % 3;
         const int m = lane & 31, h = lane >> 5;
         const int off = slot * kA1Slot + ((wave * kA1 + m + dx) * 16 + 8 * h) * 2;
-        const bf16x8 ah = *reinterpret_cast<const bf16x8*>(a1h + off);
-        const bf16x8 al = *reinterpret_cast<const bf16x8*>(a1l + off);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, w2h[t], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, w2l[t], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, w2h[t], acc, 0, 0, 0);
+        const f16x8 ah = *reinterpret_cast<const f16x8*>(a1h + off);
+        const f16x8 al = *reinterpret_cast<const f16x8*>(a1l + off);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, w2h[t], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, w2l[t], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, w2h[t], acc, 0, 0, 0);
       }
       // partial [wave][px][o2]: lane holds col o2 = lane & 31, rows (r&3) + 8 (r>>2) + 4 (lane>>5)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        part2[(wave * 32 + m) * 32 + (lane & 31)] = acc[r];
+        part2[(wave * 32 + m) * 32 + (lane & 31)] = __builtin_ldexpf(acc[r], kout2);
       }
     }
     lds_barrier();
@@ -324,23 +414,23 @@ __global__ __launch_bounds__(kThreads, 1) void v4_main(Args a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] += pv[j];
       }
-      bf16x4 h, l;
+      f16x4 h, l;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float vv = ok ? fmaxf(v[j], 0.f) : 0.f;
-        const __bf16 hb = (__bf16)vv;
-        h[j] = hb;
-        l[j] = (__bf16)(vv - (float)hb);
+        _Float16 hj, lj;
+        split16(ok ? fmaxf(v[j], 0.f) : 0.f, ka2, hj, lj);
+        h[j] = hj;
+        l[j] = lj;
       }
       const int slot = ((q % 3) + 3) % 3;
       const int off = slot * kA2Slot + (m * 64 + 4 * g) * 2;
-      *reinterpret_cast<bf16x4*>(a2h + off) = h;
-      *reinterpret_cast<bf16x4*>(a2l + off) = l;
+      *reinterpret_cast<f16x4*>(a2h + off) = h;
+      *reinterpret_cast<f16x4*>(a2l + off) = l;
       if (m < 2) {  // the ring's 2 readable pad pixels (32, 33): zeros
         const int off2 = slot * kA2Slot + ((32 + m) * 64 + 4 * g) * 2;
-        const bf16x4 z = {};
-        *reinterpret_cast<bf16x4*>(a2h + off2) = z;
-        *reinterpret_cast<bf16x4*>(a2l + off2) = z;
+        const f16x4 z = {};
+        *reinterpret_cast<f16x4*>(a2h + off2) = z;
+        *reinterpret_cast<f16x4*>(a2l + off2) = z;
       }
     }
     lds_barrier();
@@ -356,17 +446,17 @@ __global__ __launch_bounds__(kThreads, 1) void v4_main(Args a) {
           const int slot = ((r + dy - 1) % 3 + 3) % 3;
           const int px = 16 * mb + (lane & 15) + dx;
           const int off = slot * kA2Slot + (px * 64 + half * 32 + 8 * (lane >> 4)) * 2;
-          const bf16x8 ah = *reinterpret_cast<const bf16x8*>(a2h + off);
-          const bf16x8 al = *reinterpret_cast<const bf16x8*>(a2l + off);
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, w3h[qq], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, w3l[qq], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, w3h[qq], acc, 0, 0, 0);
+          const f16x8 ah = *reinterpret_cast<const f16x8*>(a2h + off);
+          const f16x8 al = *reinterpret_cast<const f16x8*>(a2l + off);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, w3h[qq], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, w3l[qq], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, w3h[qq], acc, 0, 0, 0);
         }
       }
       // partial [wave][px 16][o3 16]: col o3 = lane & 15, rows (lane >> 4) * 4 + reg
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr)
-        part3[(wave * 16 + (lane >> 4) * 4 + rr) * 16 + (lane & 15)] = acc[rr];
+        part3[(wave * 16 + (lane >> 4) * 4 + rr) * 16 + (lane & 15)] = __builtin_ldexpf(acc[rr], kout3);
     }
     lds_barrier();
     if (s >= y0 + 2 && tid < 512) {
@@ -398,7 +488,7 @@ __global__ __launch_bounds__(kThreads, 1) void v4_main(Args a) {
 size_t v4_workspace_bytes(int64_t N, int64_t H, int64_t W) {
   const size_t tables = (size_t)N * H * W * 4 * v4vol::kCh * sizeof(float);
   const size_t packed = (size_t)2 * (4 * 9 * 64 * 8 + 18 * 64 * 8) * 2;
-  return ((tables + 255) / 256) * 256 + packed;
+  return ((tables + 255) / 256) * 256 + packed + 256;  // + the scale block
 }
 
 int v4_volume_entry(const float* L, const float* R, float* out, int64_t N, int64_t C, int64_t H,
@@ -423,19 +513,23 @@ int v4_volume_entry(const float* L, const float* R, float* out, int64_t N, int64
   if (rc != SM_OK) return rc;
   float* T = static_cast<float*>(workspace);
   const size_t tables = (size_t)N * H * W * 4 * kCh * sizeof(float);
-  __bf16* P2 = reinterpret_cast<__bf16*>(static_cast<unsigned char*>(workspace) + ((tables + 255) / 256) * 256);
-  __bf16* P3 = P2 + 2 * (4 * 9 * 64 * 8);
+  _Float16* P2 = reinterpret_cast<_Float16*>(static_cast<unsigned char*>(workspace) + ((tables + 255) / 256) * 256);
+  _Float16* P3 = P2 + 2 * (4 * 9 * 64 * 8);
+  Scales* S = reinterpret_cast<Scales*>(P3 + 2 * (18 * 64 * 8));
+  if (hipMemsetAsync(S, 0, sizeof(Scales), st) != hipSuccess)
+    return fail(SM_ELAUNCH, "v4_volume: hipMemsetAsync failed");
   hipLaunchKernelGGL(v4_tables, dim3((unsigned)ceil_div(N * H * W, 256), 8), dim3(256), 0, st, L, R,
-                     ls, rs, w1, T, (int)N, (int)H, (int)W);
+                     ls, rs, w1, T, S, (int)N, (int)H, (int)W);
   rc = check_launch("v4_tables");
   if (rc != SM_OK) return rc;
-  hipLaunchKernelGGL(v4_pack, dim3(16), dim3(256), 0, st, w2, w3, P2, P3);
+  hipLaunchKernelGGL(v4_pack, dim3(1), dim3(1024), 0, st, w2, w3, b1, b2, P2, P3, S);
   rc = check_launch("v4_pack");
   if (rc != SM_OK) return rc;
   Args a;
   a.T = T;
-  a.P2 = reinterpret_cast<const bf16x8*>(P2);
-  a.P3 = reinterpret_cast<const bf16x8*>(P3);
+  a.P2 = reinterpret_cast<const f16x8*>(P2);
+  a.P3 = reinterpret_cast<const f16x8*>(P3);
+  a.S = S;
   a.b1 = b1;
   a.b2 = b2;
   a.b3 = b3;

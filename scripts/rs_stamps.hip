@@ -40,7 +40,7 @@ int main(int argc, char** argv) {
   a.pw = (int)D;
   a.mul = 1.0f / (float)C;
   bool handled = false;
-  auto run = [&]() { return smcv::h2band::band_rs_run(a, N, false, true, nullptr, &handled); };
+  auto run = [&]() { return smcv::h2band::band_rs_run(a, N, false, true, nullptr, &handled, 0); };
   for (int it = 0; it < 3; ++it) run();
   hipDeviceSynchronize();
   static unsigned long long st[4096][10];
