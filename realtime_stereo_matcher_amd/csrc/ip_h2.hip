@@ -803,6 +803,9 @@ int check_dot_args(const void* left, const void* right, const void* out, int dty
 namespace h2band {
 int band_h2db_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled);
 int band_sp_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled);
+#ifndef SMCV_RS_FUSE2
+#define SMCV_RS_FUSE2 0  // the volume-free fused pass on band_rs (else band_h2's FUSE 2)
+#endif
 int band_rs_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled,
                 int fuse);
 int band_h2db_fused_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st,
@@ -995,7 +998,10 @@ int band_h2_fused_entry(const void* left, const void* right, void* out, float* d
     return dtype == SM_F16 ? go_half(std::type_identity<__half>{}) : go_half(std::type_identity<__bf16>{});
   }
 #ifndef SMCV_NO_RS_FUSE  // (diagnostic builds: -DSMCV_NO_RS_FUSE keeps the band_h2db / band_h2 paths)
-  {  // the role-split kernel for the shapes it takes: FUSE 1 with the volume, else FUSE 2
+  // the role-split kernel for the shapes it takes, with the volume (FUSE 1: 1 % below
+  // band_h2db's FUSE 1 on cfg2); its volume-free form (FUSE 2, -DSMCV_RS_FUSE2 selects it) tied
+  // band_h2's on cfg2 and ran 6 % slower on cfg4 (profiles/r04/band_experiments/fuse_ab.jsonl)
+  if (out != nullptr || SMCV_RS_FUSE2) {
     bool done = false;
     rc = band_rs_run(a, N, mean, al4, st, &done, out != nullptr ? 1 : 2);
     if (rc != SM_OK) return rc;

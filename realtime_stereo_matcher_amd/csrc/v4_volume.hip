@@ -21,8 +21,8 @@
 // three products (hh + hl + lh: exact in fp32; the dropped lo*lo' and the lo roundings leave
 // ~3 * 2^-22 relative per product; fp32 accumulation).  The scales come from bounds computed on
 // the device before the main kernel, so the scaled values stay below 2^15 (no fp16 overflow):
-// max|W2|, max|W3| directly; |a1| <= max|b1| + max|PL| + max|PR| (v4_tables records the table
-// maxima); |a2| <= max|b2| + max_o2 sum|W2[o2]| * bound(a1).  Values far below their layer's
+// max|W2|, max|W3| directly; |a1| <= max|b1| + max|PL| + max|PR| (v4_tmax reduces the
+// tables); |a2| <= max|b2| + max_o2 sum|W2[o2]| * bound(a1).  Values far below their layer's
 // bound lose only absolute precision (the fp16 subnormal step, ~2^-39 of the bound).
 //
 // Main kernel.  A workgroup owns (n, i, a 30-pixel column strip, a band of rows) and streams down
@@ -67,12 +67,12 @@ static_assert(kShm <= 160 * 1024, "one workgroup per CU");
 __device__ __forceinline__ int ks_begin(int g) { return g == 0 ? 0 : g == 1 ? 5 : g == 2 ? 10 : 14; }
 __device__ __forceinline__ int ks_end(int g) { return g == 0 ? 5 : g == 1 ? 10 : g == 2 ? 14 : 18; }
 
-// the scale block in the workspace (after the packed weights): the table maxima (as the bits of
-// non-negative floats, atomically max'ed by v4_tables) and the four exponents v4_pack derives
+// the scale block in the workspace (after the packed weights): the four exponents v4_scales
+// derives
 struct Scales {
-  unsigned max_tl, max_tr;  // max |PL|, max |PR| over the four table variants
   int k_a1, k_w2, k_a2, k_w3;
 };
+// followed by the table maxima: one (max |PL|, max |PR|) pair per v4_tables workgroup
 
 struct Args {
   const float* T;        // tables [n][y][x][4][128]: PL, PL without dx=-1, PR, PR without dx=+1
@@ -101,14 +101,23 @@ __device__ __forceinline__ void split16(float x, int k, _Float16& hi, _Float16& 
   hi = (_Float16)v;
   lo = (_Float16)(v - (float)hi);
 }
-__device__ __forceinline__ void split8(const float (&v)[8], int k, f16x8& hi, f16x8& lo) {
+// The same split for two values at once on v_fma_mix (band_common.h's split_pair): sc = 2^k,
+// h = rn16(x sc), m = rn16(x sc - h) evaluated exactly in the mix unit and packed as (lo, hi)
+// fp16 pairs -- two VALU per value instead of the convert / subtract / convert / pack sequence.
+__device__ __forceinline__ void split_pair16(float a, float b, float sc, unsigned& h, unsigned& m) {
+  asm("v_fma_mixlo_f16 %0, %2, %4, 0\n\t"
+      "v_fma_mixhi_f16 %0, %3, %4, 0\n\t"
+      "v_fma_mixlo_f16 %1, %2, %4, -%0 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %1, %3, %4, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(h), "=&v"(m)
+      : "v"(a), "v"(b), "v"(sc));
+}
+__device__ __forceinline__ void split8(const float (&v)[8], float sc, f16x8& hi, f16x8& lo) {
+  unsigned h[4], m[4];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    _Float16 h, l;
-    split16(v[j], k, h, l);
-    hi[j] = h;
-    lo[j] = l;
-  }
+  for (int j = 0; j < 4; ++j) split_pair16(v[2 * j], v[2 * j + 1], sc, h[j], m[j]);
+  hi = __builtin_bit_cast(f16x8, (uint4){h[0], h[1], h[2], h[3]});
+  lo = __builtin_bit_cast(f16x8, (uint4){m[0], m[1], m[2], m[3]});
 }
 // exponent k with b 2^k <= 2^15 (b > 0 finite), 0 for b == 0, clamped to fp32's reach
 __device__ __forceinline__ int scale_exp(float b) {
@@ -124,18 +133,13 @@ __device__ __forceinline__ int scale_exp(float b) {
 __global__ __launch_bounds__(256) void v4_tables(const float* __restrict__ L,
                                                  const float* __restrict__ R, Strides4 ls,
                                                  Strides4 rs, const float* __restrict__ w1,
-                                                 float* __restrict__ T, Scales* __restrict__ S,
-                                                 int N, int H, int W) {
+                                                 float* __restrict__ T, int N, int H, int W) {
   __shared__ float ws[16 * 8 * 9];
   for (int e = threadIdx.x; e < 16 * 8 * 9; e += 256) ws[e] = w1[e];
   __syncthreads();
-  // (no early return: every lane reaches the maxima's wave reduction; a lane past the end
-  // computes pixel 0 again and stores nothing)
-  const int64_t pxl = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const bool live = pxl < (int64_t)N * H * W;
-  const int64_t px = live ? pxl : 0;
+  const int64_t px = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int b = blockIdx.y;
-  float ml = 0.f, mr = 0.f;  // this thread's table maxima (the a1 scale's bound)
+  if (px >= (int64_t)N * H * W) return;
   const int x = (int)(px % W);
   const int y = (int)((px / W) % H);
   const int n = (int)(px / ((int64_t)W * H));
@@ -168,103 +172,124 @@ __global__ __launch_bounds__(256) void v4_tables(const float* __restrict__ L,
         if (t % 3 == 2) prp += r;
       }
     }
-    if (live) {
-      o[o1] = pl;
-      o[kCh + o1] = pl - plm;
-      o[2 * kCh + o1] = pr;
-      o[3 * kCh + o1] = pr - prp;
-    }
-    ml = fmaxf(ml, fmaxf(fabsf(pl), fabsf(pl - plm)));
-    mr = fmaxf(mr, fmaxf(fabsf(pr), fabsf(pr - prp)));
+    o[o1] = pl;
+    o[kCh + o1] = pl - plm;
+    o[2 * kCh + o1] = pr;
+    o[3 * kCh + o1] = pr - prp;
+  }
+}
+
+// max |PL| and max |PR| over the tables (all four variants), one pair per workgroup (no
+// atomics: v4_scales reduces the pairs).  A pixel's 512 table words: 256 of L, then 256 of R.
+constexpr int kTmaxBlocks = 512;
+__global__ __launch_bounds__(256) void v4_tmax(const float* __restrict__ T, int64_t nquads,
+                                               float2* __restrict__ tmax) {
+  float ml = 0.f, mr = 0.f;
+  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < nquads; q += (int64_t)256 * gridDim.x) {
+    const f32x4v v = reinterpret_cast<const f32x4v*>(T)[q];
+    const float m = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+    if ((q & 127) < 64) ml = fmaxf(ml, m); else mr = fmaxf(mr, m);
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
     ml = fmaxf(ml, __shfl_xor(ml, o));
     mr = fmaxf(mr, __shfl_xor(mr, o));
   }
-  // non-negative floats order as their bits; NaN (bits above +inf) makes the bound non-finite,
-  // and v4_pack then leaves the scale at 2^0
-  if ((threadIdx.x & 63) == 0) {
-    atomicMax(&S->max_tl, __float_as_uint(ml));
-    atomicMax(&S->max_tr, __float_as_uint(mr));
+  __shared__ float2 wm[4];
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = make_float2(ml, mr);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float2 m = wm[0];
+    for (int w = 1; w < 4; ++w) m = make_float2(fmaxf(m.x, wm[w].x), fmaxf(m.y, wm[w].y));
+    tmax[blockIdx.x] = m;
   }
 }
 
-// ------------------------------------------------------------------------------ weight packing
-// One workgroup: the scale exponents (from the weights, the biases and the table maxima), then
-// the MFMA B fragments, scaled and split into fp16 hi / lo.  Layer 2 (32x32x16): lane l holds
-// B[k = 8 (l>>5) + j][col l&31] = W2[o2 = l&31][o1 = 8 (l>>5) + j][kd][dy][dx].  Layer 3
-// (16x16x32): step s = 2 tap + half, lane l holds B[k = 8 (l>>4) + j][col l&15] =
-// W3[o3 = l&15][o2 = k][kd = half][dy][dx].
-__global__ __launch_bounds__(1024) void v4_pack(const float* __restrict__ w2,
-                                                const float* __restrict__ w3,
-                                                const float* __restrict__ b1,
-                                                const float* __restrict__ b2,
-                                                _Float16* __restrict__ P2, _Float16* __restrict__ P3,
-                                                Scales* __restrict__ S) {
-  constexpr int n2 = 4 * 9 * 64 * 8, n3 = 18 * 64 * 8;  // = the sizes of W2, W3
-  __shared__ float red[4][32];
+// ------------------------------------------------------------------------------ scales, packing
+// v4_scales: the four exponents from the weights, the biases and the table maxima (v4_tmax).
+// v4_pack: the MFMA B fragments, scaled and split into fp16 hi / lo.  Layer 2
+// (32x32x16): lane l holds B[k = 8 (l>>5) + j][col l&31] = W2[o2 = l&31][o1 = 8 (l>>5) + j][kd]
+// [dy][dx].  Layer 3 (16x16x32): step s = 2 tap + half, lane l holds B[k = 8 (l>>4) + j]
+// [col l&15] = W3[o3 = l&15][o2 = k][kd = half][dy][dx].
+constexpr int kN2 = 4 * 9 * 64 * 8, kN3 = 18 * 64 * 8;  // = the sizes of W2, W3
+
+template <int NT>
+__device__ __forceinline__ void v4_scales(const float* __restrict__ w2, const float* __restrict__ w3,
+                                          const float* __restrict__ b1, const float* __restrict__ b2,
+                                          const float2* __restrict__ tmax, int ntmax, Scales& S) {
+  constexpr int NW = NT / 64;
+  __shared__ float red[6][NW];
   __shared__ float rows[32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  float m2 = 0.f, m3 = 0.f, mb1 = 0.f, mb2 = 0.f;
-  for (int e = tid; e < n2; e += 1024) m2 = fmaxf(m2, fabsf(w2[e]));
-  for (int e = tid; e < n3; e += 1024) m3 = fmaxf(m3, fabsf(w3[e]));
+  float m2 = 0.f, m3 = 0.f, mb1 = 0.f, mb2 = 0.f, ml = 0.f, mr = 0.f;
+  for (int e = tid; e < kN2; e += NT) m2 = fmaxf(m2, fabsf(w2[e]));
+  for (int e = tid; e < kN3; e += NT) m3 = fmaxf(m3, fabsf(w3[e]));
+  for (int e = tid; e < ntmax; e += NT) {
+    ml = fmaxf(ml, tmax[e].x);
+    mr = fmaxf(mr, tmax[e].y);
+  }
   if (tid < 16) mb1 = fabsf(b1[tid]);
   if (tid < 32) mb2 = fabsf(b2[tid]);
-  // row sums of |W2| (576 terms per output channel o2): wave o2 & 15, two rows per wave
-  if (tid < 32) rows[tid] = 0.f;
-  __syncthreads();
-  for (int o2 = wave; o2 < 32; o2 += 16) {
+  // row sums of |W2| (576 terms per output channel o2)
+  for (int o2 = wave; o2 < 32; o2 += NW) {
     float r = 0.f;
     for (int e = lane; e < 576; e += 64) r += fabsf(w2[o2 * 576 + e]);
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) r += __shfl_xor(r, o);
     if (lane == 0) rows[o2] = r;
   }
+  float v[6] = {m2, m3, mb1, mb2, ml, mr};
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    m2 = fmaxf(m2, __shfl_xor(m2, o));
-    m3 = fmaxf(m3, __shfl_xor(m3, o));
-    mb1 = fmaxf(mb1, __shfl_xor(mb1, o));
-    mb2 = fmaxf(mb2, __shfl_xor(mb2, o));
-  }
-  if (lane == 0) {
-    red[0][wave] = m2;
-    red[1][wave] = m3;
-    red[2][wave] = mb1;
-    red[3][wave] = mb2;
+  for (int q = 0; q < 6; ++q) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v[q] = fmaxf(v[q], __shfl_xor(v[q], o));
+    if (lane == 0) red[q][wave] = v[q];
   }
   __syncthreads();
-  __shared__ int ks[4];
+  __shared__ Scales ks;
   if (tid == 0) {
-    float v[4] = {0.f, 0.f, 0.f, 0.f}, rmax = 0.f;
-    for (int w = 0; w < 16; ++w)
-      for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], red[q][w]);
+    float m[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, rmax = 0.f;
+    for (int w = 0; w < NW; ++w)
+      for (int q = 0; q < 6; ++q) m[q] = fmaxf(m[q], red[q][w]);
     for (int o2 = 0; o2 < 32; ++o2) rmax = fmaxf(rmax, rows[o2]);
-    const float ba1 = v[2] + __uint_as_float(S->max_tl) + __uint_as_float(S->max_tr);
-    const float ba2 = v[3] + rmax * ba1;
-    ks[0] = scale_exp(ba1);
-    ks[1] = scale_exp(v[0]);
-    ks[2] = scale_exp(ba2);
-    ks[3] = scale_exp(v[1]);
-    S->k_a1 = ks[0];
-    S->k_w2 = ks[1];
-    S->k_a2 = ks[2];
-    S->k_w3 = ks[3];
+    const float ba1 = m[2] + m[4] + m[5];  // |a1| <= max|b1| + max|PL| + max|PR|
+    const float ba2 = m[3] + rmax * ba1;   // |a2| <= max|b2| + max_o2 sum|W2[o2]| |a1|
+    ks.k_a1 = scale_exp(ba1);
+    ks.k_w2 = scale_exp(m[0]);
+    ks.k_a2 = scale_exp(ba2);
+    ks.k_w3 = scale_exp(m[1]);
   }
   __syncthreads();
-  const int kw2 = ks[1], kw3 = ks[3];
-  for (int e = tid; e < n2 + n3; e += 1024) {
-    if (e < n2) {
+  S = ks;
+}
+
+__global__ __launch_bounds__(1024) void v4_scales_kernel(const float* __restrict__ w2,
+                                                         const float* __restrict__ w3,
+                                                         const float* __restrict__ b1,
+                                                         const float* __restrict__ b2,
+                                                         const float2* __restrict__ tmax, int ntmax,
+                                                         Scales* __restrict__ S) {
+  Scales sc;
+  v4_scales<1024>(w2, w3, b1, b2, tmax, ntmax, sc);
+  if (threadIdx.x == 0) *S = sc;
+}
+
+__global__ __launch_bounds__(256) void v4_pack(const float* __restrict__ w2,
+                                               const float* __restrict__ w3,
+                                               const Scales* __restrict__ S,
+                                               _Float16* __restrict__ P2, _Float16* __restrict__ P3) {
+  const int kw2 = S->k_w2, kw3 = S->k_w3;
+  for (int e = threadIdx.x + blockIdx.x * 256; e < kN2 + kN3; e += 256 * gridDim.x) {
+    if (e < kN2) {
       const int j = e & 7, ln = (e >> 3) & 63, tap = (e >> 9) % 9, kd = (e >> 9) / 9;
       const int o2 = ln & 31, o1 = 8 * (ln >> 5) + j;
-      split16(w2[(((o2 * 16 + o1) * 4 + kd) * 3 + tap / 3) * 3 + tap % 3], kw2, P2[e], P2[n2 + e]);
+      split16(w2[(((o2 * 16 + o1) * 4 + kd) * 3 + tap / 3) * 3 + tap % 3], kw2, P2[e], P2[kN2 + e]);
     } else {
-      const int f = e - n2;
+      const int f = e - kN2;
       const int j = f & 7, ln = (f >> 3) & 63, st = f >> 9;
       const int tap = st >> 1, half = st & 1;
       const int o3 = ln & 15, o2 = 8 * (ln >> 4) + j;
-      split16(w3[(((o3 * 32 + o2) * 2 + half) * 3 + tap / 3) * 3 + tap % 3], kw3, P3[f], P3[n3 + f]);
+      split16(w3[(((o3 * 32 + o2) * 2 + half) * 3 + tap / 3) * 3 + tap % 3], kw3, P3[f], P3[kN3 + f]);
     }
   }
 }
@@ -295,6 +320,7 @@ __global__ __launch_bounds__(kThreads, 1) void v4_main(Args a) {
 
   // ---- the layers' scale exponents (v4_pack) and the resident weights
   const int ka1 = a.S->k_a1, ka2 = a.S->k_a2;
+  const float sa1 = __builtin_ldexpf(1.0f, ka1), sa2 = __builtin_ldexpf(1.0f, ka2);
   const int kout2 = -(ka1 + a.S->k_w2), kout3 = -(ka2 + a.S->k_w3);
   f16x8 w2h[9], w2l[9];
   {
@@ -356,7 +382,7 @@ __global__ __launch_bounds__(kThreads, 1) void v4_main(Args a) {
     for (int j = 0; j < 8; ++j)
       v[j] = ok ? fmaxf(bias1[j] + (pf.pl[j >> 2][j & 3] + pf.pr[j >> 2][j & 3]), 0.f) : 0.f;
     f16x8 h, l;
-    split8(v, ka1, h, l);
+    split8(v, sa1, h, l);
     const int off = slot * kA1Slot + ((wave * kA1 + pp) * 16 + hh * 8) * 2;
     *reinterpret_cast<f16x8*>(a1h + off) = h;
     *reinterpret_cast<f16x8*>(a1l + off) = l;
@@ -395,7 +421,7 @@ __global__ __launch_bounds__(kThreads, 1) void v4_main(Args a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        part2[(wave * 32 + m) * 32 + (lane & 31)] = __builtin_ldexpf(acc[r], kout2);
+        part2[(wave * 32 + m) * 32 + (lane & 31)] = acc[r];  // (scaled: 2^-kout2)
       }
     }
     lds_barrier();
@@ -405,23 +431,24 @@ __global__ __launch_bounds__(kThreads, 1) void v4_main(Args a) {
       const int b2 = g >> 3, o2 = (4 * g) & 31;
       const int x = x0 - 1 + m;
       const bool ok = q >= 0 && q < H && x >= i && x < W;
-      float v[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = a.b2[o2 + j];
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kd = 0; kd < 4; ++kd) {
         const f32x4v pv = *reinterpret_cast<const f32x4v*>(part2 + ((4 * b2 + kd) * 32 + m) * 32 + o2);
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] += pv[j];
       }
-      f16x4 h, l;
+      // back to the unscaled sum (exact: a power of two), then the bias
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        _Float16 hj, lj;
-        split16(ok ? fmaxf(v[j], 0.f) : 0.f, ka2, hj, lj);
-        h[j] = hj;
-        l[j] = lj;
-      }
+      for (int j = 0; j < 4; ++j) v[j] = a.b2[o2 + j] + __builtin_ldexpf(v[j], kout2);
+      float r4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r4[j] = ok ? fmaxf(v[j], 0.f) : 0.f;
+      unsigned hp[2], lp[2];
+      split_pair16(r4[0], r4[1], sa2, hp[0], lp[0]);
+      split_pair16(r4[2], r4[3], sa2, hp[1], lp[1]);
+      const f16x4 h = __builtin_bit_cast(f16x4, (uint2){hp[0], hp[1]});
+      const f16x4 l = __builtin_bit_cast(f16x4, (uint2){lp[0], lp[1]});
       const int slot = ((q % 3) + 3) % 3;
       const int off = slot * kA2Slot + (m * 64 + 4 * g) * 2;
       *reinterpret_cast<f16x4*>(a2h + off) = h;
@@ -456,16 +483,17 @@ __global__ __launch_bounds__(kThreads, 1) void v4_main(Args a) {
       // partial [wave][px 16][o3 16]: col o3 = lane & 15, rows (lane >> 4) * 4 + reg
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr)
-        part3[(wave * 16 + (lane >> 4) * 4 + rr) * 16 + (lane & 15)] = __builtin_ldexpf(acc[rr], kout3);
+        part3[(wave * 16 + (lane >> 4) * 4 + rr) * 16 + (lane & 15)] = acc[rr];  // (2^-kout3)
     }
     lds_barrier();
     if (s >= y0 + 2 && tid < 512) {
       // ---- a3 = relu(b3 + sum over the 4 K groups), out = relu(b4 + w4 . a3), masked
       const int o = tid >> 4, o3 = tid & 15;  // output pixel 0..31, channel
       const int half = o >> 4, ol = o & 15;
-      float v = a.b3[o3];
+      float v = 0.f;
 #pragma unroll
       for (int g = 0; g < 4; ++g) v += part3[((2 * g + half) * 16 + ol) * 16 + o3];
+      v = a.b3[o3] + __builtin_ldexpf(v, kout3);
       v = fmaxf(v, 0.f) * a.w4[o3];
       // sum over the 16 lanes of this pixel (aligned 16-lane groups of the wave)
 #pragma unroll
@@ -488,7 +516,8 @@ __global__ __launch_bounds__(kThreads, 1) void v4_main(Args a) {
 size_t v4_workspace_bytes(int64_t N, int64_t H, int64_t W) {
   const size_t tables = (size_t)N * H * W * 4 * v4vol::kCh * sizeof(float);
   const size_t packed = (size_t)2 * (4 * 9 * 64 * 8 + 18 * 64 * 8) * 2;
-  return ((tables + 255) / 256) * 256 + packed + 256;  // + the scale block
+  // + the scale block and the per-workgroup table maxima (v4_tmax)
+  return ((tables + 255) / 256) * 256 + packed + 64 + (size_t)v4vol::kTmaxBlocks * 8;
 }
 
 int v4_volume_entry(const float* L, const float* R, float* out, int64_t N, int64_t C, int64_t H,
@@ -514,15 +543,20 @@ int v4_volume_entry(const float* L, const float* R, float* out, int64_t N, int64
   float* T = static_cast<float*>(workspace);
   const size_t tables = (size_t)N * H * W * 4 * kCh * sizeof(float);
   _Float16* P2 = reinterpret_cast<_Float16*>(static_cast<unsigned char*>(workspace) + ((tables + 255) / 256) * 256);
-  _Float16* P3 = P2 + 2 * (4 * 9 * 64 * 8);
-  Scales* S = reinterpret_cast<Scales*>(P3 + 2 * (18 * 64 * 8));
-  if (hipMemsetAsync(S, 0, sizeof(Scales), st) != hipSuccess)
-    return fail(SM_ELAUNCH, "v4_volume: hipMemsetAsync failed");
+  _Float16* P3 = P2 + 2 * kN2;
+  Scales* S = reinterpret_cast<Scales*>(P3 + 2 * kN3);
+  float2* tmax = reinterpret_cast<float2*>(reinterpret_cast<unsigned char*>(S) + 64);
   hipLaunchKernelGGL(v4_tables, dim3((unsigned)ceil_div(N * H * W, 256), 8), dim3(256), 0, st, L, R,
-                     ls, rs, w1, T, S, (int)N, (int)H, (int)W);
+                     ls, rs, w1, T, (int)N, (int)H, (int)W);
   rc = check_launch("v4_tables");
   if (rc != SM_OK) return rc;
-  hipLaunchKernelGGL(v4_pack, dim3(1), dim3(1024), 0, st, w2, w3, b1, b2, P2, P3, S);
+  hipLaunchKernelGGL(v4_tmax, dim3(kTmaxBlocks), dim3(256), 0, st, T, N * H * W * kCh, tmax);
+  rc = check_launch("v4_tmax");
+  if (rc != SM_OK) return rc;
+  hipLaunchKernelGGL(v4_scales_kernel, dim3(1), dim3(1024), 0, st, w2, w3, b1, b2, tmax, kTmaxBlocks, S);
+  rc = check_launch("v4_scales_kernel");
+  if (rc != SM_OK) return rc;
+  hipLaunchKernelGGL(v4_pack, dim3(16), dim3(256), 0, st, w2, w3, S, P2, P3);
   rc = check_launch("v4_pack");
   if (rc != SM_OK) return rc;
   Args a;

@@ -2,7 +2,9 @@
 """Diagnostic library builds for same-box A/B: libstereocv.so with one source recompiled under
 extra -D flags, written to var_so/NAME.so (select one with STEREOCV_LIB=...).
 
-    python scripts/build_variants.py NAME SOURCE.hip -DFLAG=V [...]"""
+    python scripts/build_variants.py NAME SOURCE.hip -DFLAG=V [...]
+    python scripts/build_variants.py NAME /path/other.hip:SOURCE.hip [...]   (another file in
+                                                                             SOURCE.hip's place)"""
 import os
 import subprocess
 import sys
@@ -18,8 +20,11 @@ def main():
     out_dir = os.path.join(ROOT, "build", "var")
     os.makedirs(out_dir, exist_ok=True)
     obj = os.path.join(out_dir, name + ".o")
-    srcp = os.path.join(B.CSRC, src)
-    subprocess.run([B.hipcc(), *B.CXXFLAGS, *flags, "-c", srcp, "-o", obj], check=True)
+    if ":" in src:  # another file compiled in place of a library source
+        srcp, src = src.split(":")
+    else:
+        srcp = os.path.join(B.CSRC, src)
+    subprocess.run([B.hipcc(), *B.CXXFLAGS, "-I", B.CSRC, *flags, "-c", srcp, "-o", obj], check=True)
     objs = [os.path.join(B.BUILD, os.path.basename(s)[:-4] + ".o") for s in B.sources() if os.path.basename(s) != src]
     so_dir = os.path.join(ROOT, "var_so")  # travels to the GPU box (build/ does not)
     os.makedirs(so_dir, exist_ok=True)
