@@ -136,8 +136,9 @@ def kernel_name(cfg, pipeline, algo):
         return {"valu": "dot_volume_valu", "f32": "ip_band_f32", "mfma": "ip_band_f32",
                 "h2": "band_h2", "h2db": "band_h2db",
                 "sp": "band_sp" if sp_shape else "band_h2db"}.get(algo, "band_rs" if sp_shape else "band_h2db")
-    if pipeline == "fused" and cfg.get("D", 0) <= 192:  # volume kept, one D pass: band_h2db FUSE 1
-        return "band_h2db (fused soft-argmin, volume kept)"
+    if pipeline == "fused" and cfg.get("D", 0) <= 192:  # volume kept, one D pass: FUSE 1
+        rs_shape = cfg["C"] in (16, 64) and cfg["D"] > 64 and cfg["dtype"] == torch.float32
+        return ("band_rs" if rs_shape else "band_h2db") + " (fused soft-argmin, volume kept)"
     if pipeline == "fused-novolume":
         return "band_h2 (fused soft-argmin, volume-free)"
     return "band_h2 (fused soft-argmin)" if pipeline.startswith("fused") else "band_h2"
