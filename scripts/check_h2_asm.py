@@ -8,10 +8,10 @@ kernel relies on two properties of the generated code, checked here for every in
   2. no wave ends (s_endpgm) with such a load still in flight (the L2 touches included);
   3. no `flat_*` memory instruction exists (flat ops count in vmcnt out of order, which would
      break the `vmcnt(4 (T-1))` wait that lets the output stores stay in flight);
-  4. band_h2db (ip_h2db.hip) and band_sp (ip_sp.hip) have no scratch access at all: a spill
-     reload counts in vmcnt (band_sp's loads are compiler-tracked; the other checks find no
-     inline-asm loads in it, and the scratch check is what applies there) and
-     would wait for the feature loads in flight.
+  4. band_h2db (ip_h2db.hip), band_sp (ip_sp.hip) and band_rs (ip_rs.hip) have no scratch
+     access at all: a spill reload counts in vmcnt (band_sp's and band_rs's loads are
+     compiler-tracked; the other checks find no inline-asm loads in them, and the scratch check
+     is what applies there) and would wait for the feature loads in flight.
 A may-pending dataflow over the kernel's basic blocks carries each load to every instruction it
 can reach before a vmcnt wait.
 
@@ -26,7 +26,8 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "realtime_stereo_matcher_amd", "csrc")
-SRCS = [os.path.join(CSRC, "ip_h2.hip"), os.path.join(CSRC, "ip_h2db.hip"), os.path.join(CSRC, "ip_sp.hip")]
+SRCS = [os.path.join(CSRC, "ip_h2.hip"), os.path.join(CSRC, "ip_h2db.hip"), os.path.join(CSRC, "ip_sp.hip"),
+        os.path.join(CSRC, "ip_rs.hip")]
 
 
 def regs(tok):
@@ -43,7 +44,7 @@ def kernels(asm_text):
     only those loads are hand-counted (the compiler waits for its own)."""
     out, cur, in_asm = [], None, False
     for ln, line in enumerate(asm_text.splitlines(), 1):
-        if re.match(r"^_ZN4smcv6h2band(7band_h2|9band_h2db|7band_sp).*:", line):
+        if re.match(r"^_ZN4smcv6h2band(7band_h2|9band_h2db|7band_sp|7band_rs).*:", line):
             cur = (line.split(":")[0], [])
             out.append(cur)
             continue
@@ -143,8 +144,8 @@ def check(asm_text):
                         changed = True
         rep = []
         for i, b in enumerate(blocks):
-            # no scratch at all in band_h2db (volume and fused) and band_sp
-            no_scr = "9band_h2db" in name or "7band_sp" in name
+            # no scratch at all in band_h2db (volume and fused), band_sp and band_rs
+            no_scr = "9band_h2db" in name or "7band_sp" in name or "7band_rs" in name
             transfer(b, ins_state[i], rep, no_scratch=no_scr)
         bad += [f"{name}:{r}" for r in rep]
     return bad
@@ -158,16 +159,21 @@ def main():
         srcs = [os.path.join(ROOT, "scripts", "experimental", "ip_stamps.hip")]
         args.append("-DSMCV_STAMPS")
     bad, n = [], 0
-    for src in srcs:
-        stem = os.path.basename(src)[:-4]
-        with tempfile.TemporaryDirectory() as td:
+    # the sources compile concurrently (device code only: the asm is all that is scanned)
+    with tempfile.TemporaryDirectory() as td:
+        procs = []
+        for k, src in enumerate(srcs):
+            out = os.path.join(td, f"k{k}.s")
             cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++20", "--offload-arch=gfx950", *args, "-I",
-                   os.path.join(ROOT, "include"), "-c", src, "--save-temps", "-o",
-                   os.path.join(td, "h2.o")]
-            subprocess.run(cmd, cwd=td, check=True, capture_output=True)
-            asm = open(os.path.join(td, f"{stem}-hip-amdgcn-amd-amdhsa-gfx950.s")).read()
-        bad += check(asm)
-        n += len(kernels(asm))
+                   os.path.join(ROOT, "include"), "--cuda-device-only", "-S", src, "-o", out]
+            procs.append((subprocess.Popen(cmd, cwd=td, stdout=subprocess.PIPE, stderr=subprocess.PIPE), out))
+        for p, out in procs:
+            _, err = p.communicate()
+            if p.returncode != 0:
+                raise SystemExit(err.decode()[-2000:])
+            asm = open(out).read()
+            bad += check(asm)
+            n += len(kernels(asm))
     for b in bad[:40]:
         print(b)
     print(f"{n} kernels checked, {len(bad)} problems")
