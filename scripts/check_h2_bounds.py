@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Host-side replay of the band kernels' indexing (csrc/ip_h2.hip), run before any GPU launch of
-a changed indexing scheme:   python scripts/check_h2_bounds.py
+"""Host-side replay of the band kernels' indexing (csrc/ip_h2.hip; the folded ring of
+csrc/ip_rs.hip), run before any GPU launch of a changed indexing scheme:
+    python scripts/check_h2_bounds.py
 
 1. every stage lane's feature loads and L2 touches, for every step of every workgroup, stay
    inside the feature tensor and inside the lane's channel group -- for the (N, D, H, W) kernels
@@ -232,8 +233,62 @@ def check_stores(N, H, W, D, G=1, layout=0, ncu=256):
     return bad
 
 
+def check_rs_ring(T):
+    """band_rs's ring (csrc/ip_rs.hip): T-1 chunks of 4 KB per compute wave, chunk m at m*4096;
+    block t (a = T-2-t) writes element i of lane (lr, hh) -- local disparity 32 (a+1) + u - c_i,
+    u = lr - 4 hh -- at wb + (a+1) 4096 - 128 c_i - 512 (wb = 512 + 128 u + 4 lr), except the
+    folded blocks T-1 (a = -1, into chunk 0) and 0 (a = T-2, into chunk T-2):
+    ((32768 + 128 u + 4 lr - 128 c_i) & 4095) + (0 | (T-2) 4096).  Written in the order T-1, 0,
+    1, ..., T-2, every cell (chunk m, row r, pixel lr) must end up holding local disparity
+    32 m + r; every address stays in [0, (T-1) 4096); ds_write_b32 lane groups (0-31, 32-63) are
+    conflict free; the readouts (rows 8 qq + rl, 16 B at 16 cl) stay inside their chunk.
+    Returns (wrong cells, out-of-range accesses, conflicted lane groups)."""
+    size = (T - 1) * KSLOT
+    ring = {}
+    oob = conf = 0
+    for t in [T - 1] + list(range(T - 1)):
+        a = T - 2 - t
+        for i in range(16):
+            ci = (i & 3) + 8 * (i >> 2)
+            addrs = []
+            for lane in range(64):
+                lr, hh = lane & 31, lane >> 5
+                u = lr - 4 * hh
+                if a in (-1, T - 2):
+                    ad = ((32768 + 128 * u + 4 * lr - 128 * ci) & 4095) + (0 if a == -1 else (T - 2) * KSLOT)
+                else:
+                    ad = (512 + 128 * u + 4 * lr) + (a + 1) * KSLOT - 128 * ci - 512
+                if not 0 <= ad < size:
+                    oob += 1
+                    continue
+                ring[ad] = 32 * (a + 1) + u - ci  # the element's local disparity
+                addrs.append((lane, ad))
+            for half in (0, 1):
+                banks = [(ad // 4) % 32 for ln, ad in addrs if ln >> 5 == half]
+                if len(set(banks)) != len(banks):
+                    conf += 1
+    wrong = 0
+    for m in range(T - 1):
+        for r in range(32):
+            for lr in range(32):
+                if ring.get(m * KSLOT + r * 128 + 4 * lr) != 32 * m + r:
+                    wrong += 1
+    for m in range(T - 1):
+        for lane in range(64):
+            rl, cl = lane >> 3, lane & 7
+            for qq in range(4):
+                ad = m * KSLOT + qq * 1024 + rl * 128 + 16 * cl
+                if not (m * KSLOT <= ad and ad + 16 <= (m + 1) * KSLOT):
+                    oob += 1
+    return wrong, oob, conf
+
+
 if __name__ == "__main__":
     fails = 0
+    for T in (3, 5, 7):
+        w, o, c = check_rs_ring(T)
+        print(f"band_rs ring T={T}: wrong cells {w}, out-of-range {o}, conflicted lane groups {c}")
+        fails += w + o + c
     for layout in (0, 1):
         for T in (2, 3, 5, 7):
             b, c = check_shear(T, layout)
