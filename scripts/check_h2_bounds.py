@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Host-side replay of the band kernels' indexing (csrc/ip_h2.hip; the folded ring of
-csrc/ip_rs.hip), run before any GPU launch of a changed indexing scheme:
+"""Host-side replay of the band kernels' indexing (csrc/ip_h2.hip; the rings of csrc/ip_h2db.hip
+and csrc/ip_rs.hip), run before any GPU launch of a changed indexing scheme:
     python scripts/check_h2_bounds.py
 
 1. every stage lane's feature loads and L2 touches, for every step of every workgroup, stay
@@ -283,8 +283,45 @@ def check_rs_ring(T):
     return wrong, oob, conf
 
 
+def check_h2db_ring(T):
+    """band_h2db's epilogue ring (csrc/ip_h2db.hip): 2 slots x 4 KB per wave, chunk m in slot m & 1;
+    element i of lane (lr, hh) in block t (a = T-2-t) at yi = 4096 + 128 (u - c_i) + 4 lr, XOR
+    4096 when a is odd.  Replays the epilogue's order -- for t = T-1 .. 0: write block t, (store
+    chunk a-1 from registers), read chunk a -- and checks every read cell of chunk a holds local
+    disparity 32 a + row, every access stays in [0, 8192), the writes are conflict free per
+    32-lane half.  Returns (wrong cells, out-of-range accesses, conflicted lane groups)."""
+    ring = {}
+    wrong = oob = conf = 0
+    for t in range(T - 1, -1, -1):
+        a = T - 2 - t
+        for i in range(16):
+            ci = (i & 3) + 8 * (i >> 2)
+            banks = {0: [], 1: []}
+            for lane in range(64):
+                lr, hh = lane & 31, lane >> 5
+                u = lr - 4 * hh
+                yi = 4096 + 128 * (u - ci) + 4 * lr
+                ad = (yi ^ 4096) if (a & 1) else yi
+                if not 0 <= ad < 2 * KSLOT:
+                    oob += 1
+                    continue
+                ring[ad] = 32 * (a + 1) + u - ci
+                banks[hh].append((ad // 4) % 32)
+            conf += sum(len(set(b)) != len(b) for b in banks.values())
+        if a >= 0:
+            for r in range(32):
+                for x in range(32):
+                    if ring.get((a & 1) * KSLOT + r * 128 + 4 * x) != 32 * a + r:
+                        wrong += 1
+    return wrong, oob, conf
+
+
 if __name__ == "__main__":
     fails = 0
+    for T in (3, 5, 7):
+        w, o, c = check_h2db_ring(T)
+        print(f"band_h2db ring T={T}: wrong cells {w}, out-of-range {o}, conflicted lane groups {c}")
+        fails += w + o + c
     for T in (3, 5, 7):
         w, o, c = check_rs_ring(T)
         print(f"band_rs ring T={T}: wrong cells {w}, out-of-range {o}, conflicted lane groups {c}")
