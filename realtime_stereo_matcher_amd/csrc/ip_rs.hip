@@ -118,6 +118,9 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
 
   const Sched sched(args.nwork, args.npass);
   if (sched.none) return;  // the whole workgroup leaves together
+#ifdef SMCV_RS_PRIO  // diagnostics: 1 the compute waves, 2 the memory waves issue at priority 1
+  if constexpr ((SMCV_RS_PRIO == 1) == isC) __builtin_amdgcn_s_setprio(1);
+#endif
   const int nitems = sched.nitems;
   auto witem = [&](int i) -> Work {
     return decode_fd((unsigned)sched.item_fd(min(i, nitems - 1), args.fd_np), args, DMAX);
