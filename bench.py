@@ -127,8 +127,8 @@ def pair_mfma_flops(cfg):
 def kernel_name(cfg, pipeline, algo):
     if cfg["op"] == "concat":
         return "shifted_rows_kernel" if pipeline == "interweave" else "concat_kernel"
-    if cfg["op"] == "groupwise":
-        return "band_h2 (NGHWD, bf16)"
+    if cfg["op"] == "groupwise":  # 16-bit features, 16-channel group steps, one D pass: band_rs
+        return "band_rs (NGHWD, bf16)"
     if cfg["op"] in ("inner_product", "correlation") and pipeline == "separate":
         # fp32 aligned rows with C = 16 or 64 and > 64 disparities per pass (cfg2, cfg4): the
         # role-split band kernel (AUTO, rs); other shapes the double-buffered one

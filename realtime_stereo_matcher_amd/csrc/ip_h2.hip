@@ -803,6 +803,7 @@ int check_dot_args(const void* left, const void* right, const void* out, int dty
 namespace h2band {
 int band_h2db_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled);
 int band_sp_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled);
+int band_rs_gw_run(const Args& a, int64_t N, int dtype, hipStream_t st, bool* handled);
 #ifndef SMCV_RS_FUSE2
 #define SMCV_RS_FUSE2 0  // the volume-free fused pass on band_rs (else band_h2's FUSE 2)
 #endif
@@ -924,6 +925,11 @@ int band_h2_groupwise_entry(const void* left, const void* right, float* out, int
   a.cpg = (int)(C / G);
   a.mul = 1.0f / (float)a.cpg;
   hipStream_t st = as_stream(stream);
+  {  // 16-bit features with 16-channel group steps: the role-split kernel
+    bool done = false;
+    rc = band_rs_gw_run(a, N, dtype, st, &done);
+    if (done || rc != SM_OK) return rc;
+  }
   SM_DISPATCH_DTYPE(dtype, T0, {
     using T = typename std::conditional<std::is_same<T0, bf16_t>::value, __bf16, T0>::type;
     return by_tmax(a.pw, [&](auto tm) {

@@ -76,13 +76,13 @@ constexpr int kThreads = 2 * 64 * kCW;
 constexpr int kKC = 16;                // channels per step (one 32x32x16 k-step)
 constexpr int kSlot = 32 * 32 * 4;     // one ring chunk: 32 d x 32 x fp32
 
-template <int TMAX, int FUSE = 0>
+template <int TMAX, int FUSE = 0, int NPL = 2>
 struct Geo {
   static constexpr int DMAX = 32 * (TMAX - 1);
   static constexpr int RW = kXT + DMAX;    // right-window rows
   static constexpr int ROWS = RW + kXT;    // + left-tile rows
   static constexpr int PLANE = ROWS * 32;  // one fp16 plane: rows of 16 channels
-  static constexpr int BUF = 2 * PLANE;    // h + m planes of one step
+  static constexpr int BUF = NPL * PLANE;  // the planes of one step (fp32: h + m; 16-bit: one)
   static constexpr int GROUPS = ROWS / 4;
   static constexpr int ITEMS = 2 * GROUPS;
   // one compute wave's ring (the volume-free fused pass has none)
@@ -102,17 +102,19 @@ constexpr int chunk_lo(int ks, int T, int NKS) { return (ks * (T - 1) + NKS - 1)
 // checks, restarts and barriers, all decided on workgroup-uniform data); what each does between
 // the barriers is selected at compile time, so neither role's registers (the accumulators, the
 // load sets) are live in the other's code.
-template <bool CW, bool MEAN, int TMAX, int NKS, int NSETS, int FUSE>
+template <bool CW, bool MEAN, int TMAX, int NKS, int NSETS, int FUSE, typename TI, bool GW>
 __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
   using namespace roles;
-  using G = roles::Geo<TMAX, FUSE>;
+  constexpr bool F32 = std::is_same<TI, float>::value;  // else fp16 / bf16: exact products
+  using G = roles::Geo<TMAX, FUSE, F32 ? 2 : 1>;
+  static_assert(F32 || FUSE == 0, "the fused passes of 16-bit features run on band_h2");
   constexpr bool VOL = FUSE != 2;  // the volume is written (FUSE 0, 1)
   constexpr int T = TMAX;
   constexpr int DMAX = G::DMAX;
   static_assert(T >= 3, "blocks 0 and T-1 are distinct and fold into distinct chunks");
   constexpr bool isC = CW;
-  const float* __restrict__ L = static_cast<const float*>(args.L);
-  const float* __restrict__ R = static_cast<const float*>(args.R);
+  const TI* __restrict__ L = static_cast<const TI*>(args.L);
+  const TI* __restrict__ R = static_cast<const TI*>(args.R);
   const int cpg = args.cpg, H = args.H, W = args.W, D = args.D;
   const Strides4 ls = args.ls, rs = args.rs;
 
@@ -147,12 +149,13 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
 
   // NSETS feature-load register sets: the loads of step j land in set j % NSETS, issued
   // NSETS - 1 steps before the step that stages them
-  f32x4v sv[NSETS][8];
+  using QT = typename Quad<TI>::type;  // 4 pixels of one channel row: 16 B fp32, 8 B 16-bit
+  QT sv[NSETS][8];
   bool okp[NSETS];
   auto load = [&](int set, const Work& k, int ks) __attribute__((always_inline)) {
     const int px = isR ? k.js + 4 * g : k.x0 + 4 * g - G::RW;
     okp[set] = active && px >= 0 && px < W;
-    if constexpr (SMCV_RS_ABLATE & 4) {
+    if constexpr ((SMCV_RS_ABLATE & 4) && F32) {
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk) {
         sv[set][kk] = f32x4v{1.f, -1.f, 0.5f, 2.f};
@@ -162,9 +165,9 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
     }
     int pxc = min(max(px, 0), W - 4);  // pad groups: the nearest valid group
     if constexpr (SMCV_RS_ABLATE & 32) pxc = 4 * (lane & 7);  // L2-resident lines only
-    const float* p = (isR ? R + (int64_t)k.n * rs.n + (int64_t)k.y * rs.h
-                          : L + (int64_t)k.n * ls.n + (int64_t)k.y * ls.h) +
-                     pxc + (SMCV_RS_ABLATE & 32 ? 0 : (int64_t)(ks * kKC + 8 * ch) * cs);
+    const TI* p = (isR ? R + (int64_t)k.n * rs.n + (int64_t)k.y * rs.h
+                       : L + (int64_t)k.n * ls.n + (int64_t)k.y * ls.h) +
+                  pxc + (SMCV_RS_ABLATE & 32 ? 0 : ((int64_t)k.g * cpg + ks * kKC + 8 * ch) * cs);
     int64_t csl = SMCV_RS_ABLATE & 32 ? 0 : cs;
     asm volatile("" : "+v"(csl));
 #pragma unroll
@@ -179,6 +182,28 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
   // split of its four pixels into the h and m planes.
   auto stage = [&](int set, unsigned buf) __attribute__((always_inline)) {
     if constexpr (SMCV_RS_ABLATE & 16) return;
+    if constexpr (!F32) {
+      // 16-bit features as they are: pixel p's 8 channels -> 16 B of the one plane (pad groups
+      // zeroed: they reach only cells x < d or columns x >= W)
+      u32x2 qv[8];
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) qv[kk] = okp[set] ? sv[set][kk] : u32x2{0u, 0u};
+      unsigned o0 = buf + (unsigned)swz(4 * g, ch);
+      asm volatile("" : "+v"(o0));
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        uint4 w;
+        unsigned* pw_ = reinterpret_cast<unsigned*>(&w);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {  // channels 2j (low half), 2j+1 (high half) of pixel p
+          const unsigned lo = p < 2 ? qv[2 * j].x : qv[2 * j].y;
+          const unsigned hi = p < 2 ? qv[2 * j + 1].x : qv[2 * j + 1].y;
+          pw_[j] = __builtin_amdgcn_perm(hi, lo, (p & 1) ? 0x07060302u : 0x05040100u);
+        }
+        if (active) *reinterpret_cast<uint4*>(smem + (o0 ^ (32u * p))) = w;
+      }
+      return;
+    } else {
     f32x4v(&sv_)[8] = sv[set];
     float m0 = 0.f, m1 = 0.f;
 #pragma unroll
@@ -201,6 +226,7 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
         *reinterpret_cast<uint4*>(smem + off) = wh;
         *reinterpret_cast<uint4*>(smem + G::PLANE + off) = wm;
       }
+    }
     }
   };
   // maxima words: set s (0..3) at MAXW + 8 s: max|L|, max|R|
@@ -241,16 +267,26 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
   // wb = ring + 512 + 128 u + 4 lr (>= ring: u >= -4), an immediate offset per element.  Block
   // T-1 (a = -1) folds chunk -1 into chunk 0 and block 0 (a = T-2) chunk T-1 into chunk T-2:
   // ((128 (u - c_i) + 4 lr) mod 4096) within the chunk.
+  //
+  // GW (groupwise, (N, G, H, W, D) output): the ring is [32 px][DMAX d] fp32 per compute wave
+  // (RS = 4 DMAX bytes per pixel), the layout of the output's pixel records, so a wave's 32
+  // pixels read out as 1-KB contiguous pieces.  Element address ring + lr RS + 4 dl =
+  // wbg + 128 (a + 1) - 4 c_i - 16 with wbg = ring + 16 + lr (RS + 4) - 16 hh; the straddling
+  // blocks fold into chunk 0 / chunk T-2 with dl mod 32 (the same cells as in NDHW terms).
+  // ds_write_b32: bank = (lr RS / 4 + dl) mod 32 = (const + lr) mod 32, conflict free.
+  constexpr int RS = 4 * DMAX;
   const int u = lr - 4 * hh;
   const unsigned ring = lds_addr(smem) + (unsigned)(rw * G::RINGW);
   // lane constants of the ring writes: the plain base, and the 16 folded addresses of the two
   // straddling blocks (one per element row c_i; block 0 adds chunk T-2's offset)
-  const unsigned wb = ring + (unsigned)(512 + 128 * u + 4 * lr);
+  const unsigned wb = GW ? ring + (unsigned)(16 + lr * (RS + 4) - 16 * hh)
+                         : ring + (unsigned)(512 + 128 * u + 4 * lr);
   unsigned fold[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int ci = (i & 3) + 8 * (i >> 2);
-    fold[i] = ring + ((unsigned)(32768 + 128 * u + 4 * lr - 128 * ci) & 4095u);
+    fold[i] = GW ? ring + (unsigned)(lr * RS) + 4u * ((unsigned)(u - ci) & 31u)
+                 : ring + ((unsigned)(32768 + 128 * u + 4 * lr - 128 * ci) & 4095u);
   }
   // SPEC: the segment is scaled (kk != 0) or holds cells x < d (R pad rows, forced to 0); the
   // plain form is one ds_write_b32 per element with an immediate offset and no vector ALU work
@@ -267,19 +303,15 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
       float val = acc[t][i];
       if constexpr (MEAN) val *= args.mul;
       if constexpr (SPEC) {
-        val = __builtin_ldexpf(val, p_kk);
+        if constexpr (F32) val = __builtin_ldexpf(val, p_kk);
         val = jl + 32 * t + ci >= 0 ? val : 0.f;  // R pad rows: cells x < d
       }
+      constexpr int fold_off = a == -1 ? 0 : GW ? (T - 2) * 128 : (T - 2) * kSlot;
+      const int imm = GW ? 128 * (a + 1) - 4 * ci - 16 : (a + 1) * kSlot - 128 * ci - 512;
       if constexpr (a == -1 || a == T - 2) {
-        asm volatile("ds_write_b32 %0, %1 offset:%2"
-                     :
-                     : "v"(fl), "v"(val), "n"(a == -1 ? 0 : (T - 2) * kSlot)
-                     : "memory");
+        asm volatile("ds_write_b32 %0, %1 offset:%2" : : "v"(fl), "v"(val), "n"(fold_off) : "memory");
       } else {
-        asm volatile("ds_write_b32 %0, %1 offset:%2"
-                     :
-                     : "v"(wbl), "v"(val), "n"((a + 1) * kSlot - 128 * ci - 512)
-                     : "memory");
+        asm volatile("ds_write_b32 %0, %1 offset:%2" : : "v"(wbl), "v"(val), "n"(imm) : "memory");
       }
     }
   };
@@ -323,8 +355,17 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
   const int rl = lane >> 3, cl = lane & 7;
   // chunk m of the ring: rows 8 qq + rl, pixels 4 cl .. 4 cl + 3 -> out[n, dp + 32 m + row, y,
   // x0 + 32 rw + 4 cl ..]
+  // GW: unit m is the wave ring's bytes [4096 m, 4096 (m + 1)), four 1-KB pieces, lane l at
+  // 16 l of a piece: byte o is pixel o / RS, disparity (o % RS) / 4 of the wave's 32 pixels
   auto drain_read = [&]<int m>(f32x4v(&vp)[4]) __attribute__((always_inline)) {
     if constexpr ((SMCV_RS_ABLATE & 2) || !VOL) return;
+    if constexpr (GW) {
+      unsigned rb = ring + 16u * (unsigned)lane;
+      asm volatile("" : "+v"(rb));
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) vp[qq] = lds_load4(rb + (unsigned)(m * 4096 + qq * 1024));
+      return;
+    }
     int rr = rl, cc = cl;
     asm volatile("" : "+v"(rr), "+v"(cc));
     const unsigned rb = ring + (unsigned)(rr * 128 + 16 * cc);
@@ -333,6 +374,28 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
   };
   auto drain_store = [&]<int m>(const f32x4v(&vp)[4]) __attribute__((always_inline)) {
     if constexpr ((SMCV_RS_ABLATE & 2) || !VOL) return;
+    if constexpr (GW) {
+      const __amdgpu_buffer_rsrc_t rsrc =
+          __builtin_amdgcn_make_buffer_rsrc(p_ob, (short)0, p_bytes, 0x00020000);
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const unsigned o = (unsigned)(m * 4096 + qq * 1024) + 16u * (unsigned)ln;
+        unsigned off;
+        if (p_full) {  // the wave's 32 pixel records are one contiguous range of the output
+          off = o;
+        } else {
+          const unsigned px = o / (unsigned)RS, dd = (o % (unsigned)RS) / 4u;
+          const unsigned bad = (unsigned)(pw.x0 + 32 * rw + (int)px >= W || (int)dd >= pw.Dp) << 31;
+          off = (px * (unsigned)D + dd) * 4u | bad;
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, vp[qq]), rsrc, off, 0,
+            SMCV_NT_STORE ? 2 : 0);
+      }
+      return;
+    }
     int rr = rl, cc = cl;
     asm volatile("" : "+v"(rr), "+v"(cc));
     float* cb = p_ob + (int64_t)(32 * m) * plane_stride;
@@ -375,9 +438,15 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
     p_kk = -(kL + kR);
     p_special = p_kk != 0 || k.js < 0;
     p_bytes = valid ? (int)0x80000000 : 0;
-    p_full = k.Dp == DMAX && k.x0 + kXT <= W;
-    p_ob = static_cast<float*>(args.out) +
-           (((int64_t)k.n * D + k.dp) * plane_stride + (int64_t)k.y * W + k.x0 + 32 * rw);
+    if constexpr (GW) {  // (N, G, H, W, D): the wave's first pixel record, from disparity dp
+      p_full = k.Dp == DMAX && D == DMAX && k.x0 + kXT <= W;
+      p_ob = static_cast<float*>(args.out) +
+             ((((int64_t)k.n * args.G + k.g) * H + k.y) * W + k.x0 + 32 * rw) * D + k.dp;
+    } else {
+      p_full = k.Dp == DMAX && k.x0 + kXT <= W;
+      p_ob = static_cast<float*>(args.out) +
+             (((int64_t)k.n * D + k.dp) * plane_stride + (int64_t)k.y * W + k.x0 + 32 * rw);
+    }
   };
 
   auto barrier = []() __attribute__((always_inline)) {
@@ -426,7 +495,26 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
     [[maybe_unused]] f32x4v pv[2][4];
     if constexpr (isC && npre > 0) drain_read.template operator()<c0>(pv[0]);
     if constexpr (isC && npre > 1) drain_read.template operator()<c0 + 1>(pv[1]);
-    if constexpr (isC) {
+    if constexpr (isC && !F32) {  // 16-bit features: one exact product per block
+      using FV = typename std::conditional<std::is_same<TI, __bf16>::value, bf16x8, f16x8>::type;
+      const unsigned char* ab = smem + bm + 32 * rw * 32 + swz(lr, hh);
+      const unsigned char* bb = smem + bm + (G::RW + 32 * rw) * 32 + swz(lr, hh);
+      const FV bh = *reinterpret_cast<const FV*>(bb);
+      FV ah[2];
+      ah[0] = *reinterpret_cast<const FV*>(ab);
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        if (t + 1 < T) ah[(t + 1) & 1] = *reinterpret_cast<const FV*>(ab + 1024 * (t + 1));
+        const f32x16 c0v = KS == 0 ? f32x16{} : acc[t];
+        if constexpr (std::is_same<TI, __bf16>::value)
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[t & 1], bh, c0v, 0, 0, 0);
+        else
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[t & 1], bh, c0v, 0, 0, 0);
+      }
+      if constexpr (npre > 0) drain_store.template operator()<c0>(pv[0]);
+      if constexpr (npre > 1) drain_store.template operator()<c0 + 1>(pv[1]);
+      if constexpr (SMCV_RS_DRAIN_C) drain_range.template operator()<c0 + npre, c1>();
+    } else if constexpr (isC) {
       const unsigned char* ab = smem + bm + 32 * rw * 32 + swz(lr, hh);
       const unsigned char* bb = smem + bm + (G::RW + 32 * rw) * 32 + swz(lr, hh);
       const f16x8 bh = *reinterpret_cast<const f16x8*>(bb);
@@ -461,7 +549,7 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
       if constexpr (ss == 0) mx = 0.f;  // the staged step opens its segment
       stage(sset, sb);
       RS_STAMP(7);
-      if constexpr (ss == NKS - 1) {  // the staged segment is complete: its maxima
+      if constexpr (ss == NKS - 1 && F32) {  // the staged segment is complete: its maxima
         if (it + sd < nitems) publish_max((it + sd) & 3);
       }
       if constexpr (!SMCV_RS_DRAIN_C)
@@ -474,13 +562,15 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
   };
 
   // exact fp32 FMA path for a segment holding a non-finite value or out of the scale range
+  // (16-bit features never take it: no scale, and their maxima stay 0)
   auto slow_segment = [&](const Work& k) __attribute__((always_inline)) {
+    if constexpr (!F32 || GW) return;
     if constexpr (FUSE != 0) slow_softargmin_f32<MEAN>(args, k, tid, kThreads);
     if constexpr (!VOL) return;
     const float mul = MEAN ? args.mul : 1.0f;
     float* out = static_cast<float*>(args.out);
-    const float* lrow = L + (int64_t)k.n * ls.n + (int64_t)k.y * ls.h;
-    const float* rrow = R + (int64_t)k.n * rs.n + (int64_t)k.y * rs.h;
+    const float* lrow = static_cast<const float*>(args.L) + (int64_t)k.n * ls.n + (int64_t)k.y * ls.h;
+    const float* rrow = static_cast<const float*>(args.R) + (int64_t)k.n * rs.n + (int64_t)k.y * rs.h;
     for (int idx = tid; idx < k.Dp * kXT; idx += kThreads) {
       const int dl = idx / kXT, x = k.x0 + idx % kXT, d = k.dp + dl;
       if (x >= W) continue;
@@ -506,7 +596,7 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
       load(GS0 % NSETS, wq[0], 0);
       mx = 0.f;
       stage(GS0 % NSETS, bm);
-      if constexpr (NKS == 1) publish_max(it & 3);
+      if constexpr (NKS == 1 && F32) publish_max(it & 3);
 #pragma unroll
       for (int k = 1; k < NSETS; ++k) load((GS0 + k) % NSETS, wq[k / NKS], k % NKS);
       // A (re)start may land its loads in other registers than the steady-state loop, which
@@ -597,18 +687,20 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
 
 // FUSE 0: the volume; 1: the volume and its soft-argmin; 2: the soft-argmin only (no ring, no
 // volume stores)
-template <bool MEAN, int TMAX, int NKS, int NSETS, int FUSE>
+// TI: the feature type (fp32: the split; fp16 / bf16: as they are); GW: the groupwise
+// (N, G, H, W, D) fp32 output (else (N, D, H, W) in the feature type's fp32 form)
+template <bool MEAN, int TMAX, int NKS, int NSETS, int FUSE, typename TI = float, bool GW = false>
 __global__ __launch_bounds__(roles::kThreads, 1) void band_rs(Args args) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) < roles::kCW)
-    rs_role<true, MEAN, TMAX, NKS, NSETS, FUSE>(args, smem);
+    rs_role<true, MEAN, TMAX, NKS, NSETS, FUSE, TI, GW>(args, smem);
   else
-    rs_role<false, MEAN, TMAX, NKS, NSETS, FUSE>(args, smem);
+    rs_role<false, MEAN, TMAX, NKS, NSETS, FUSE, TI, GW>(args, smem);
 }
 
-template <bool MEAN, int TMAX, int NKS, int NSETS, int FUSE>
+template <bool MEAN, int TMAX, int NKS, int NSETS, int FUSE, typename TI = float, bool GW = false>
 int launch_rs(Args a, int64_t N, hipStream_t st) {
-  using G = roles::Geo<TMAX, FUSE>;
+  using G = roles::Geo<TMAX, FUSE, std::is_same<TI, float>::value ? 2 : 1>;
   a.tiles = (int)ceil_div(a.W, kXT);
   const int64_t nwork = (int64_t)a.tiles * a.H * N * a.G * a.npass;
   if (nwork > INT32_MAX / 64) return fail(SM_EINVAL, "band kernel: too much work for one launch");
@@ -617,7 +709,7 @@ int launch_rs(Args a, int64_t N, hipStream_t st) {
   a.fd_tiles = make_fastdiv((unsigned)a.tiles);
   a.fd_g = make_fastdiv((unsigned)a.G);
   a.fd_h = make_fastdiv((unsigned)a.H);
-  auto kern = band_rs<MEAN, TMAX, NKS, NSETS, FUSE>;
+  auto kern = band_rs<MEAN, TMAX, NKS, NSETS, FUSE, TI, GW>;
   static std::atomic<unsigned long long> lds_done{0};
   const int dev = stream_device(st);
   if (int rc = ensure_lds_limit(reinterpret_cast<const void*>(kern), (int)G::SHM, dev, lds_done))
@@ -665,6 +757,40 @@ int band_rs_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t 
   using T7 = std::integral_constant<int, 7>;
   if (a.pw <= 128) return nks == 1 ? go(T5{}, I1{}) : go(T5{}, I4{});
   return nks == 1 ? go(T7{}, I1{}) : go(T7{}, I4{});
+}
+
+#ifndef SMCV_RS_GW
+#define SMCV_RS_GW 1  // groupwise volumes of 16-bit features on band_rs (0: band_h2)
+#endif
+// Groupwise volume (mean over C/G channels, (N, G, H, W, D) fp32) of fp16 / bf16 features on the
+// role-split kernel; *handled = false when the shape is not one it takes: 4-element aligned
+// rows, C/G a multiple of 16 (one or more 16-channel steps per group: 1, 2 or 4), one D pass of
+// 65..192 disparities with D % 4 == 0 (whole 16-B quads of a pixel record).
+int band_rs_gw_run(const Args& a, int64_t N, int dtype, hipStream_t st, bool* handled) {
+  *handled = false;
+  const int nks = a.cpg / 16;
+  if (!SMCV_RS_GW || (dtype != SM_F16 && dtype != SM_BF16) || a.W < 4 || a.cpg % 16 != 0 ||
+      (nks != 1 && nks != 2 && nks != 4) || a.npass != 1 || a.pw <= 64 || a.pw > 192 ||
+      a.D % 4 != 0)
+    return SM_OK;
+  *handled = true;
+  auto go = [&](auto tm, auto nk, auto ti) {
+    constexpr int TM = decltype(tm)::value, NK = decltype(nk)::value;
+    using TI = typename decltype(ti)::type;
+    constexpr int NS = NK == 1 ? 2 : 4;
+    return launch_rs<true, TM, NK, NS, 0, TI, true>(a, N, st);
+  };
+  auto by_t = [&](auto ti) {
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I4 = std::integral_constant<int, 4>;
+    using T5 = std::integral_constant<int, 5>;
+    using T7 = std::integral_constant<int, 7>;
+    if (a.pw <= 128)
+      return nks == 1 ? go(T5{}, I1{}, ti) : nks == 2 ? go(T5{}, I2{}, ti) : go(T5{}, I4{}, ti);
+    return nks == 1 ? go(T7{}, I1{}, ti) : nks == 2 ? go(T7{}, I2{}, ti) : go(T7{}, I4{}, ti);
+  };
+  return dtype == SM_F16 ? by_t(std::type_identity<__half>{}) : by_t(std::type_identity<__bf16>{});
 }
 
 }  // namespace h2band

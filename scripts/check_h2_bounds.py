@@ -316,8 +316,44 @@ def check_h2db_ring(T):
     return wrong, oob, conf
 
 
+def check_rs_gw_ring(T):
+    """band_rs's groupwise ring (GW): [32 px][DMAX d] fp32 per compute wave (RS = 4 DMAX bytes
+    per pixel); element i of lane (lr, hh), block t (a = T-2-t) at wbg + 128 (a+1) - 4 c_i - 16
+    with wbg = 16 + lr (RS + 4) - 16 hh, the straddling blocks at lr RS + 4 ((u - c_i) mod 32)
+    (+ 128 (T-2) for block 0).  Written T-1, 0, ..., T-2: every cell (px, d) must hold local
+    disparity d; accesses stay in [0, 32 RS); ds_write_b32 32-lane groups conflict free."""
+    DMAX = 32 * (T - 1)
+    RS = 4 * DMAX
+    ring = {}
+    oob = conf = 0
+    for t in [T - 1] + list(range(T - 1)):
+        a = T - 2 - t
+        for i in range(16):
+            ci = (i & 3) + 8 * (i >> 2)
+            banks = {0: [], 1: []}
+            for lane in range(64):
+                lr, hh = lane & 31, lane >> 5
+                u = lr - 4 * hh
+                if a in (-1, T - 2):
+                    ad = lr * RS + 4 * ((u - ci) & 31) + (0 if a == -1 else 128 * (T - 2))
+                else:
+                    ad = 16 + lr * (RS + 4) - 16 * hh + 128 * (a + 1) - 4 * ci - 16
+                if not 0 <= ad < 32 * RS:
+                    oob += 1
+                    continue
+                ring[ad] = (lr, 32 * (a + 1) + u - ci)
+                banks[hh].append((ad // 4) % 32)
+            conf += sum(len(set(b)) != len(b) for b in banks.values())
+    wrong = sum(ring.get(px * RS + 4 * d) != (px, d) for px in range(32) for d in range(DMAX))
+    return wrong, oob, conf
+
+
 if __name__ == "__main__":
     fails = 0
+    for T in (3, 5, 7):
+        w, o, c = check_rs_gw_ring(T)
+        print(f"band_rs groupwise ring T={T}: wrong cells {w}, out-of-range {o}, conflicted lane groups {c}")
+        fails += w + o + c
     for T in (3, 5, 7):
         w, o, c = check_h2db_ring(T)
         print(f"band_h2db ring T={T}: wrong cells {w}, out-of-range {o}, conflicted lane groups {c}")

@@ -182,3 +182,26 @@ def test_sp_cfg4_bench_launch_shape(algo):
     vol = F.correlation_volume(L, R, 256, algo=algo)
     torch.cuda.synchronize()
     _check_rows(vol, host(L), host(R), 256, (0, 541, 1079), mean=True)
+
+
+# groupwise volumes of 16-bit features on the role-split kernel ((N, G, H, W, D) fp32 output,
+# the ring in pixel-record layout): group steps of 16 / 32 / 64 channels, D = 68..192 (D < DMAX
+# takes the masked readout), ragged W, several pairs; exact products, so within 1e-4 of the
+# fp64 oracle on the dtype-rounded features
+GW_SHAPES = [(1, 256, 3, 960, 192, 8), (2, 64, 2, 260, 100, 4), (1, 128, 2, 200, 68, 4),
+             (1, 64, 3, 132, 128, 1), (1, 32, 2, 388, 160, 2), (3, 128, 1, 64, 192, 2)]
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16], ids=["bf16", "f16"])
+@pytest.mark.parametrize("shape", GW_SHAPES, ids=[str(s) for s in GW_SHAPES])
+def test_rs_groupwise_16bit(shape, dt):
+    from realtime_stereo_matcher_amd import functional as F
+
+    n, c, h, w, D, G = shape
+    l, r = _feats(hash(shape) % 991, (n, c, h, w))
+    L = torch.from_numpy(l).cuda().to(dt)
+    R = torch.from_numpy(r).cuda().to(dt)
+    got = host(F.groupwise_volume(L, R, G, D))
+    assert got.shape == (n, G, h, w, D)
+    want = O.groupwise(host(L), host(R), G, D)
+    np.testing.assert_allclose(got, want, atol=TOL, rtol=0)
