@@ -57,7 +57,7 @@ ARITH_SPLIT = ("fp32 features as a per-item power-of-two scaled, round-to-neares
 
 CONFIGS = {
     "cfg2": dict(C=64, H=540, W=960, D=192, dtype=torch.float32, op="inner_product", regress=True,
-                 global_batch=32, chunk=8, dname="f32",
+                 global_batch=32, chunk=32, dname="f32",
                  workload="BASELINE configs[1]: mobile_stereo_net inner_product CV, 1/4-res KITTI "
                           "540x960, C=64, D=192, fp32 + soft-argmin regression"),
     "cfg3": dict(C=256, H=540, W=960, D=192, G=8, dtype=torch.bfloat16, op="groupwise",
@@ -65,7 +65,7 @@ CONFIGS = {
                  workload="BASELINE configs[2]: groupwise cost volume, G=8 C=256 D=192 at 540x960, "
                           "bf16 in, fp32 (N,G,H,W,D) out, MFMA path"),
     "cfg4": dict(C=16, H=1080, W=1920, D=256, dtype=torch.float32, op="correlation", regress=True,
-                 global_batch=32, chunk=4, dname="f32",
+                 global_batch=32, chunk=32, dname="f32",
                  workload="BASELINE configs[3]: mobile_disp_net_c correlation CV, full-res 1080x1920, "
                           "C=16, D=256, fp32 + soft-argmin, global batch 32 sharded over the GPUs"),
     "cfg5": dict(C=128, H=540, W=960, D=64, dtype=torch.float16, op="concat", regress=False,

@@ -283,8 +283,11 @@ __device__ __forceinline__ int exp_of(float x) { return __builtin_amdgcn_frexp_e
 // 64-pixel last tile of a 960-pixel row would idle half the time; rotating each complete
 // aligned 8-segment block by the round spreads the short tiles over all workgroups (the set
 // of segments in flight per round, and so the L2 sharing, is unchanged).
+#ifndef SMCV_SCHED_PHASE
+#define SMCV_SCHED_PHASE 0
+#endif
 struct Sched {
-  int gi, gsz, sbeg, scnt, nitems, npass;
+  int gi, gsz, sbeg, scnt, nitems, npass, phase;
   bool rot, none;
   __device__ __forceinline__ Sched(int nwork, int np) {
     const int grp = blockIdx.x & 7;
@@ -298,13 +301,21 @@ struct Sched {
     none = gi >= scnt;  // the whole workgroup leaves together
     nitems = none ? 0 : ((scnt - gi + gsz - 1) / gsz) * np;
     rot = (gsz & 7) == 0;
+    // diagnostic: start each XCD's walk at a different point of its range (a rotation, so every
+    // segment is still taken once), so the eight XCDs' streams are not a fixed stride apart
+    phase = SMCV_SCHED_PHASE == 0 ? 0 : (int)(((long long)scnt * grp / (8 * SMCV_SCHED_PHASE)) & ~7);
+  }
+  __device__ __forceinline__ int rotate(int local) const {
+    if (SMCV_SCHED_PHASE == 0) return local;
+    local += phase;
+    return local >= scnt ? local - scnt : local;
   }
   __device__ __forceinline__ int item_fd(int i, const FastDiv& fnp) const {
     const int si = (int)fdiv((unsigned)i, fnp);
     const int p = i - si * npass;
     const int j = gi + si * gsz;
     const int b = j & ~7;
-    const int seg = sbeg + ((rot && b + 8 <= scnt) ? (b | ((j + si) & 7)) : j);
+    const int seg = sbeg + rotate((rot && b + 8 <= scnt) ? (b | ((j + si) & 7)) : j);
     return seg * npass + p;
   }
   __device__ __forceinline__ int item(int i) const {
@@ -312,7 +323,7 @@ struct Sched {
     const int p = i - si * npass;
     const int j = gi + si * gsz;
     const int b = j & ~7;
-    const int seg = sbeg + ((rot && b + 8 <= scnt) ? (b | ((j + si) & 7)) : j);
+    const int seg = sbeg + rotate((rot && b + 8 <= scnt) ? (b | ((j + si) & 7)) : j);
     return seg * npass + p;
   }
 };

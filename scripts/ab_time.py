@@ -36,6 +36,11 @@ def ops():
         # name: (setup -> callable, pairs per launch, algorithmic bytes per pair)
         "cfg2": (lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192))(*feats((8, 64, 540, 960), torch.float32)),
                  8, 663552000),
+        # the bench's launch since pairs per launch = the rank's whole batch (32 at N = 1)
+        "cfg2_b32": (lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192))(*feats((32, 64, 540, 960), torch.float32)),
+                     32, 663552000),
+        "cfg4_b32": (lambda: (lambda L, R: lambda: F.correlation_volume(L, R, 256))(*feats((32, 16, 1080, 1920), torch.float32)),
+                     32, 2388787200),
         "cfg2_h2": (lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="h2"))(*feats((8, 64, 540, 960), torch.float32)),
                     8, 663552000),
         "cfg2_h2db": (lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="h2db"))(*feats((8, 64, 540, 960), torch.float32)),

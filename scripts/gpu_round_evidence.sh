@@ -14,6 +14,6 @@ bash scripts/gpu_evidence.sh "$TAG/ev" "cfg2:--config cfg2" "cfg2_fused:--config
   "cfg2_fused_novolume_f16:--config cfg2 --pipeline fused-novolume --features f16" \
   "cfg3:--config cfg3" "cfg4:--config cfg4" "cfg4_fused_novolume:--config cfg4 --pipeline fused-novolume" \
   "cfg5:--config cfg5" "cfg5_interweave:--config cfg5 --pipeline interweave" || exit 5
-bash scripts/gpu_sq.sh "$TAG/sq" "cfg2 cfg4" || exit 6
+bash scripts/gpu_sq.sh "$TAG/sq" "cfg2_b32 cfg4_b32" || exit 6
 timeout -k 10 120 python scripts/v4_bench.py > "$OUT/v4.json" 2> "$OUT/v4.err" || exit 7
 cat "$OUT/v4.json"

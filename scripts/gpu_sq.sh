@@ -1,5 +1,5 @@
 #!/bin/bash
-# SQ counters of the cfg2 band kernels (8 pairs per launch, scripts/ab_time.py): where the waves'
+# SQ counters of the band kernels (scripts/ab_time.py ops; cfg2_b32 / cfg4_b32 = the bench launch): where the waves'
 # cycles go (parked at waitcnt / barrier, issue-stalled, issuing by instruction class), MFMA
 # busy, LDS conflicts, clock.   bash scripts/gpu_sq.sh TAG "op1 op2 ..."
 cd "$GRAFT_REPO_ROOT" || exit 1

@@ -137,51 +137,59 @@ def test_sp_strided_inputs(algo):
     np.testing.assert_allclose(got, O.inner_product(l[:, ::2], r[:, 1::2], 192), atol=TOL, rtol=0)
 
 
-def _check_rows(vol, ln, rn, D, rows, mean=False):
+def _check_rows(vol, L, R, D, rows, mean=False):
+    """Rows of every pair of ``vol`` against the oracle; copies only those rows to the host."""
     for n in range(vol.shape[0]):
         for y in rows:
             fn = O.correlation_mean if mean else O.inner_product
-            ref = fn(ln[n:n + 1, :, y:y + 1], rn[n:n + 1, :, y:y + 1], D)
+            ref = fn(host(L[n:n + 1, :, y:y + 1]), host(R[n:n + 1, :, y:y + 1]), D)
             np.testing.assert_allclose(host(vol[n:n + 1, :, y:y + 1]), ref, atol=TOL, rtol=0,
                                        err_msg=f"pair {n} row {y}")
 
 
+# bench.py CONFIGS: cfg2 and cfg4 launch the rank's whole batch (32 pairs at N = 1) at once
+BENCH_PAIRS = 32
+
+
 @pytest.mark.parametrize("algo", ALGOS)
 def test_sp_cfg2_bench_launch_shape(algo):
-    """The bench's launch: 8 cfg2 pairs (8x64x540x960 fp32, D = 192) in ONE launch.  Rows of
+    """The bench's launch: the whole cfg2 global batch, 32 pairs (32x64x540x960 fp32, D = 192;
+    a 12.7 GB volume) in ONE launch.  Rows of
     EVERY pair (first, last and the pair boundaries of the persistent schedule) against the
     oracle, the x < d triangle exactly zero, and the soft-argmin of every sampled row."""
     from realtime_stereo_matcher_amd import functional as F
 
     g = torch.Generator(device="cuda").manual_seed(3)
-    L = torch.randn(8, 64, 540, 960, device="cuda", generator=g)
-    R = torch.randn(8, 64, 540, 960, device="cuda", generator=g)
+    L = torch.randn(BENCH_PAIRS, 64, 540, 960, device="cuda", generator=g)
+    R = torch.randn(BENCH_PAIRS, 64, 540, 960, device="cuda", generator=g)
     vol = F.inner_product_volume(L, R, 192, algo=algo)
     disp = F.soft_argmin(vol)
     torch.cuda.synchronize()
-    ln, rn = host(L), host(R)
-    _check_rows(vol, ln, rn, 192, (0, 1, 270, 538, 539))
-    for n in range(8):
+    _check_rows(vol, L, R, 192, (0, 1, 270, 538, 539))
+    for n in range(BENCH_PAIRS):
         got = host(vol[n:n + 1, :, 100:101])
         np.testing.assert_allclose(host(disp[n:n + 1, :, 100:101]).reshape(-1),
                                    O.softargmin(got).reshape(-1), atol=TOL, rtol=0)
     tri = torch.arange(960, device="cuda")[None, :] < torch.arange(192, device="cuda")[:, None]
-    for n in range(8):
+    for n in range(BENCH_PAIRS):
         assert not vol[n].permute(1, 0, 2)[:, tri].any()
 
 
 @pytest.mark.parametrize("algo", ALGOS)
 def test_sp_cfg4_bench_launch_shape(algo):
-    """The bench's cfg4 launch: 4 pairs of 16x1080x1920 fp32, correlation D = 256 (two passes of
-    128 per segment) in one launch; rows of every pair against the oracle."""
+    """The bench's cfg4 launch: the whole global batch, 32 pairs of 16x1080x1920 fp32, correlation
+    D = 256 (two passes of 128 per segment; a 68 GB volume, element offsets past 2^32) in one
+    launch; rows of every pair against the oracle."""
     from realtime_stereo_matcher_amd import functional as F
 
     g = torch.Generator(device="cuda").manual_seed(4)
-    L = torch.randn(4, 16, 1080, 1920, device="cuda", generator=g)
-    R = torch.randn(4, 16, 1080, 1920, device="cuda", generator=g)
+    L = torch.randn(BENCH_PAIRS, 16, 1080, 1920, device="cuda", generator=g)
+    R = torch.randn(BENCH_PAIRS, 16, 1080, 1920, device="cuda", generator=g)
     vol = F.correlation_volume(L, R, 256, algo=algo)
     torch.cuda.synchronize()
-    _check_rows(vol, host(L), host(R), 256, (0, 541, 1079), mean=True)
+    _check_rows(vol, L, R, 256, (0, 541, 1079), mean=True)
+    del vol
+    torch.cuda.empty_cache()
 
 
 # groupwise volumes of 16-bit features on the role-split kernel ((N, G, H, W, D) fp32 output,
