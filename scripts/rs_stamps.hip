@@ -1,6 +1,6 @@
 // Diagnostic driver: per-role, per-phase s_memtime breakdown of the role-split band kernel
 // (csrc/ip_rs.hip) on the cfg2 launch (8 pairs of 64 x 540 x 960 fp32, D = 192; arguments
-// N C D H W MEAN for other shapes), and the spread of the waves' finishing times per XCD.
+// N C D H W MEAN WARM for other shapes), and the spread of the waves' finishing times per XCD.
 //   hipcc -O3 -std=c++20 --offload-arch=gfx950 -DSMCV_RS_STAMPS -Iinclude scripts/rs_stamps.hip -o rs_stamps
 // Stamps execute only in this build (never in libstereocv.so).
 #include "../realtime_stereo_matcher_amd/csrc/common.hip"
@@ -20,6 +20,7 @@ int main(int argc, char** argv) {
                 D = argc > 3 ? atoi(argv[3]) : 192, H = argc > 4 ? atoi(argv[4]) : 540,
                 W = argc > 5 ? atoi(argv[5]) : 960;
   const bool mean = argc > 6 && atoi(argv[6]) != 0;
+  const int warm = argc > 7 ? atoi(argv[7]) : 3;  // launches before the stamped one
   const size_t nin = N * C * H * W, nout = N * D * H * W;
   float *L, *R, *O;
   hipMalloc(&L, nin * 4);
@@ -45,7 +46,7 @@ int main(int argc, char** argv) {
   a.mul = mean ? 1.0f / (float)C : 1.0f;
   bool handled = false;
   auto run = [&]() { return smcv::h2band::band_rs_run(a, N, mean, true, nullptr, &handled, 0); };
-  for (int it = 0; it < 3; ++it) run();
+  for (int it = 0; it < warm; ++it) run();
   hipDeviceSynchronize();
   static unsigned long long st[4096][10];
   memset(st, 0, sizeof(st));
@@ -73,7 +74,8 @@ int main(int argc, char** argv) {
     ++nw[role];
     for (int p = 0; p < 10; ++p) sum[p] += st[w][p];
   }
-  printf("band_rs rc=%d handled=%d: %.1f us, waves C %d M %d\n", rc, (int)handled, ms * 1e3, nw[0], nw[1]);
+  printf("band_rs rc=%d handled=%d: %.1f us after %d launches, waves C %d M %d\n", rc, (int)handled, ms * 1e3,
+         warm, nw[0], nw[1]);
   for (int r = 0; r < 2; ++r) {
     double tt = 0;
     for (int p = 5 * r; p < 5 * r + 5; ++p) tt += sum[p];
@@ -100,8 +102,9 @@ int main(int argc, char** argv) {
     std::sort(all.begin(), all.end());
     if (all.empty()) continue;
     const size_t n = all.size();
-    printf(" %s lifetime cycles: min %.0f p10 %.0f median %.0f p90 %.0f max %.0f\n", r ? "memory" : "compute",
-           all[0], all[n / 10], all[n / 2], all[9 * n / 10], all[n - 1]);
+    printf(" %s lifetime cycles: min %.0f p10 %.0f median %.0f p90 %.0f max %.0f (clock %.2f GHz: max / event time)\n",
+           r ? "memory" : "compute", all[0], all[n / 10], all[n / 2], all[9 * n / 10], all[n - 1],
+           all[n - 1] / (ms * 1e6));
     printf("  per XCD mean/max:");
     for (int x = 0; x < 8; ++x) printf(" %.0f/%.0f", xsum[x] / (xn[x] ? xn[x] : 1), xmax[x]);
     printf("\n");
