@@ -139,8 +139,10 @@ def kernel_name(cfg, pipeline, algo):
     if pipeline == "fused" and cfg.get("D", 0) <= 192:  # volume kept, one D pass: FUSE 1
         rs_shape = cfg["C"] in (16, 64) and cfg["D"] > 64 and cfg["dtype"] == torch.float32
         return ("band_rs" if rs_shape else "band_h2db") + " (fused soft-argmin, volume kept)"
-    if pipeline == "fused-novolume":
-        return "band_h2 (fused soft-argmin, volume-free)"
+    if pipeline == "fused-novolume":  # fp32, one D pass: band_rs FUSE 2; else band_h2 FUSE 2
+        rs_shape = (cfg["C"] in (16, 64) and 64 < cfg["D"] <= 192 and cfg["dtype"] == torch.float32
+                    and not cfg.get("autocast"))
+        return ("band_rs" if rs_shape else "band_h2") + " (fused soft-argmin, volume-free)"
     return "band_h2 (fused soft-argmin)" if pipeline.startswith("fused") else "band_h2"
 
 

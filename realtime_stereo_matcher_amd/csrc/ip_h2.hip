@@ -805,7 +805,7 @@ int band_h2db_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_
 int band_sp_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled);
 int band_rs_gw_run(const Args& a, int64_t N, int dtype, hipStream_t st, bool* handled);
 #ifndef SMCV_RS_FUSE2
-#define SMCV_RS_FUSE2 0  // the volume-free fused pass on band_rs (else band_h2's FUSE 2)
+#define SMCV_RS_FUSE2 1  // the one-pass volume-free fused pass on band_rs (0: band_h2's FUSE 2)
 #endif
 int band_rs_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled,
                 int fuse);
@@ -1005,9 +1005,11 @@ int band_h2_fused_entry(const void* left, const void* right, void* out, float* d
   }
 #ifndef SMCV_NO_RS_FUSE  // (diagnostic builds: -DSMCV_NO_RS_FUSE keeps the band_h2db / band_h2 paths)
   // the role-split kernel for the shapes it takes, with the volume (FUSE 1: 1 % below
-  // band_h2db's FUSE 1 on cfg2); its volume-free form (FUSE 2, -DSMCV_RS_FUSE2 selects it) tied
-  // band_h2's on cfg2 and ran 6 % slower on cfg4 (profiles/r04/band_experiments/fuse_ab.jsonl)
-  if (out != nullptr || SMCV_RS_FUSE2) {
+  // band_h2db's FUSE 1 on cfg2) and, for one D pass, without it (FUSE 2: 103.3 against band_h2's
+  // 111.3-111.7 us per pair on 32-pair cfg2 launches, a tie at 8 pairs,
+  // profiles/r04/band_experiments/fuse2_b32.jsonl; on cfg4's two passes it ran 6 % slower,
+  // fuse_ab.jsonl, so D > 192 stays on band_h2)
+  if (out != nullptr || (SMCV_RS_FUSE2 && a.npass == 1)) {
     bool done = false;
     rc = band_rs_run(a, N, mean, al4, st, &done, out != nullptr ? 1 : 2);
     if (rc != SM_OK) return rc;

@@ -729,6 +729,31 @@ def test_fused_volume_free_multipass_exact_segments(kind, mean):
     np.testing.assert_allclose(got, want, atol=TOL, rtol=0, equal_nan=True)
 
 
+@pytest.mark.parametrize("mean", [False, True])
+@pytest.mark.parametrize("kind", ["nonfinite", "tiny"])
+def test_fused_volume_free_one_pass_exact_segments(kind, mean):
+    """One D pass (D = 160, C = 64: the role-split kernel's volume-free form) on segments that
+    take the exact fp32 path: +-inf / NaN features, or a scale the fp16 split cannot reach.  The
+    volume-free disparity equals the volume-kept call's bit for bit (NaN where it is NaN), and
+    that one is the fp64 soft-argmin of its volume."""
+    from realtime_stereo_matcher_amd import functional as F
+
+    l, r = _feats(26 if kind == "nonfinite" else 27, (2, 64, 3, 320))
+    if kind == "nonfinite":
+        l[0, 5, 0, 300] = np.inf
+        l[1, 0, 1, 7] = -np.inf
+        r[0, 3, 1, 100] = np.nan
+        r[1, 9, 2, 3] = np.inf
+    else:
+        l, r = (l * 1e-28).astype(np.float32), (r * 1e-8).astype(np.float32)
+    L, R = dev(l), dev(r)
+    vol, disp = F.inner_product_soft_argmin(L, R, 160, mean=mean)
+    none, disp2 = F.inner_product_soft_argmin(L, R, 160, mean=mean, keep_volume=False)
+    assert none is None
+    np.testing.assert_array_equal(host(disp2), host(disp))
+    np.testing.assert_allclose(host(disp), O.softargmin(host(vol)), atol=TOL, rtol=0, equal_nan=True)
+
+
 def test_cfg2_fused_full_size():
     """cfg2 through the fused kernel: the volume equals the volume op's bit for bit, the
     disparity is the fp64 soft-argmin of that volume, with or without the volume written."""
