@@ -805,7 +805,8 @@ int band_h2db_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_
 int band_sp_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled);
 int band_rs_gw_run(const Args& a, int64_t N, int dtype, hipStream_t st, bool* handled);
 #ifndef SMCV_RS_FUSE2
-#define SMCV_RS_FUSE2 1  // the one-pass volume-free fused pass on band_rs (0: band_h2's FUSE 2)
+#define SMCV_RS_FUSE2 1  // the one-pass volume-free fused pass on band_rs (0: band_h2's FUSE 2;
+                         // 2, diagnostic: also the D passes + merge)
 #endif
 int band_rs_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled,
                 int fuse);
@@ -1009,7 +1010,7 @@ int band_h2_fused_entry(const void* left, const void* right, void* out, float* d
   // 111.3-111.7 us per pair on 32-pair cfg2 launches, a tie at 8 pairs,
   // profiles/r04/band_experiments/fuse2_b32.jsonl; on cfg4's two passes it ran 6 % slower,
   // fuse_ab.jsonl, so D > 192 stays on band_h2)
-  if (out != nullptr || (SMCV_RS_FUSE2 && a.npass == 1)) {
+  if (out != nullptr || (SMCV_RS_FUSE2 && (a.npass == 1 || SMCV_RS_FUSE2 == 2))) {
     bool done = false;
     rc = band_rs_run(a, N, mean, al4, st, &done, out != nullptr ? 1 : 2);
     if (rc != SM_OK) return rc;

@@ -43,6 +43,8 @@ def ops():
                      32, 2388787200),
         "cfg2_fused_nv_b32": (lambda: (lambda L, R: lambda: F.inner_product_soft_argmin(L, R, 192, keep_volume=False))(
             *feats((32, 64, 540, 960), torch.float32)), 32, 267494400),
+        "cfg4_fused_nv_b32": (lambda: (lambda L, R: lambda: F.inner_product_soft_argmin(L, R, 256, mean=True, keep_volume=False))(
+            *feats((32, 16, 1080, 1920), torch.float32)), 32, 273715200),
         "cfg2_h2": (lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="h2"))(*feats((8, 64, 540, 960), torch.float32)),
                     8, 663552000),
         "cfg2_h2db": (lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="h2db"))(*feats((8, 64, 540, 960), torch.float32)),
