@@ -1008,8 +1008,9 @@ int band_h2_fused_entry(const void* left, const void* right, void* out, float* d
   // the role-split kernel for the shapes it takes, with the volume (FUSE 1: 1 % below
   // band_h2db's FUSE 1 on cfg2) and, for one D pass, without it (FUSE 2: 103.3 against band_h2's
   // 111.3-111.7 us per pair on 32-pair cfg2 launches, a tie at 8 pairs,
-  // profiles/r04/band_experiments/fuse2_b32.jsonl; on cfg4's two passes it ran 6 % slower,
-  // fuse_ab.jsonl, so D > 192 stays on band_h2)
+  // profiles/r04/band_experiments/fuse2_b32.jsonl; on cfg4's two passes it ran 4-7 % slower,
+  // fuse_ab.jsonl, fuse2_cfg4_b32.jsonl: 381 against 364-366 us per pair at 32 pairs, so D > 192
+  // stays on band_h2)
   if (out != nullptr || (SMCV_RS_FUSE2 && (a.npass == 1 || SMCV_RS_FUSE2 == 2))) {
     bool done = false;
     rc = band_rs_run(a, N, mean, al4, st, &done, out != nullptr ? 1 : 2);
