@@ -86,7 +86,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=None,
                     help="pairs per GPU per step (weak scaling; overrides --global-batch)")
     ap.add_argument("--chunk", type=int, default=None, help="pairs per kernel launch")
-    ap.add_argument("--algo", default="auto", choices=["auto", "rs", "sp", "h2", "h2db", "f32", "mfma", "valu"],
+    ap.add_argument("--algo", default="auto", choices=["auto", "sl", "rs", "h2", "h2db", "f32", "mfma", "valu"],
                     help="cfg2 volume kernel of --pipeline separate")
     ap.add_argument("--pipeline", default="separate",
                     choices=["separate", "fused", "fused-novolume", "interweave"])
@@ -129,21 +129,25 @@ def kernel_name(cfg, pipeline, algo):
         return "shifted_rows_kernel" if pipeline == "interweave" else "concat_kernel"
     if cfg["op"] == "groupwise":  # 16-bit features, 16-channel group steps, one D pass: band_rs
         return "band_rs (NGHWD, bf16)"
+    f32 = cfg["dtype"] == torch.float32 and not cfg.get("autocast")
+    # fp32 aligned rows with C = 16 or 64: the role-split band kernel for the volume (AUTO, rs);
+    # the fused passes on the sliding-window one (one D pass of 65..192 disparities, or C = 16
+    # with two passes of <= 128, D <= 256)
+    sl_shape = f32 and cfg["C"] in (16, 64) and (64 < cfg["D"] <= 192 or (cfg["C"] == 16 and 192 < cfg["D"] <= 256))
+    rs_shape = f32 and cfg["C"] in (16, 64) and cfg["D"] > 64
     if cfg["op"] in ("inner_product", "correlation") and pipeline == "separate":
-        # fp32 aligned rows with C = 16 or 64 and > 64 disparities per pass (cfg2, cfg4): the
-        # role-split band kernel (AUTO, rs); other shapes the double-buffered one
-        sp_shape = cfg["C"] in (16, 64) and cfg["D"] > 64
         return {"valu": "dot_volume_valu", "f32": "ip_band_f32", "mfma": "ip_band_f32",
                 "h2": "band_h2", "h2db": "band_h2db",
-                "sp": "band_sp" if sp_shape else "band_h2db"}.get(algo, "band_rs" if sp_shape else "band_h2db")
-    if pipeline == "fused" and cfg.get("D", 0) <= 192:  # volume kept, one D pass: FUSE 1
-        rs_shape = cfg["C"] in (16, 64) and cfg["D"] > 64 and cfg["dtype"] == torch.float32
-        return ("band_rs" if rs_shape else "band_h2db") + " (fused soft-argmin, volume kept)"
-    if pipeline == "fused-novolume":  # fp32, one D pass: band_rs FUSE 2; else band_h2 FUSE 2
-        rs_shape = (cfg["C"] in (16, 64) and 64 < cfg["D"] <= 192 and cfg["dtype"] == torch.float32
-                    and not cfg.get("autocast"))
-        return ("band_rs" if rs_shape else "band_h2") + " (fused soft-argmin, volume-free)"
-    return "band_h2 (fused soft-argmin)" if pipeline.startswith("fused") else "band_h2"
+                "sl": "band_sl" if sl_shape else "band_h2db"}.get(algo, "band_rs" if rs_shape else "band_h2db")
+    if pipeline == "fused":  # volume kept: FUSE 1 (one D pass); D > 192: the two kernels
+        if not f32:
+            return "band_h2 (fused soft-argmin, volume kept)"
+        if cfg["D"] > 192:  # the volume kernel (AUTO), then the regression
+            return "band_rs" if rs_shape else "band_h2db"
+        return ("band_sl" if sl_shape else "band_h2db") + " (fused soft-argmin, volume kept)"
+    if pipeline == "fused-novolume":  # fp32: band_sl FUSE 2; 16-bit features: band_h2 FUSE 2
+        return ("band_sl" if sl_shape else "band_h2") + " (fused soft-argmin, volume-free)"
+    return "band_h2"
 
 
 def arithmetic(cfg, pipeline, algo):
@@ -312,6 +316,24 @@ def check_numerics(cfg, a, L, R, last):
         if disp is not None:
             # the regression of each sampled volume row against its fp64 soft-argmin
             out["all_pairs_max_abs_err_regression"] = worst_d
+    elif cfg["op"] in ("inner_product", "correlation") and disp is not None:
+        # volume-free fused launch: one row of every pair's disparity against the exact fp64
+        # pipeline (oracle volume, fp64 soft-argmin); per-pixel bar as above (torch fp32's own
+        # deviation on the first pair's rows, at least 1e-4), mean (EPE difference) within 1e-4
+        pairs, worst_d, means = [], 0.0, []
+        for j in range(disp.shape[0]):
+            y = (37 * j + 11) % H
+            ly = host(L[s0 + j:s0 + j + 1, :, y:y + 1].float())
+            ry = host(R[s0 + j:s0 + j + 1, :, y:y + 1].float())
+            ref = (O.inner_product(ly, ry, D) if cfg["op"] == "inner_product"
+                   else O.correlation_mean(ly, ry, D)).astype(np.float64)
+            dd = np.abs(host(disp[j:j + 1, :, y:y + 1]).astype(np.float64) - O.softargmin(ref))
+            worst_d = max(worst_d, float(dd.max()))
+            means.append(float(dd.mean()))
+            pairs.append([s0 + j, y])
+        out["all_pairs_checked"] = pairs
+        out["all_pairs_max_abs_err_disparity"] = worst_d
+        out["all_pairs_mean_abs_err_disparity"] = sum(means) / len(means)
     out["tolerance"] = 0.0 if cfg["op"] == "concat" else 1e-4
     return out
 

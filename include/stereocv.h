@@ -68,14 +68,18 @@ enum sm_ip_algo {
                             the current step's MFMA phase (fp32, aligned rows; else MFMA_H2; the
                             fallback of MFMA_SP, MFMA_RS and AUTO) */
   /* 9: reserved (store waves fed through an LDS queue, retired in round 4: slower) */
-  SM_IP_MFMA_SP = 10     /* software-pipelined band kernel: one workgroup per CU, two accumulator
-                            sets, the previous segment's shear and stores spread over the current
-                            segment's steps (fp32, aligned rows, C = 16 or 64, D in 65..192 per
-                            pass; other shapes: MFMA_H2DB) */,
-  SM_IP_MFMA_RS = 11     /* role-split band kernel: per SIMD a compute wave (MFMAs, shear ring,
-                            volume stores) and a memory wave (feature loads and staging); same
-                            shapes as MFMA_SP, others: MFMA_H2DB.  AUTO's choice for the shapes
-                            it takes */
+  /* 10: reserved (one-wave-per-SIMD software-pipelined band, retired in round 5: slower than
+         MFMA_RS; source under scripts/experimental/) */
+  SM_IP_MFMA_RS = 11,    /* role-split band kernel: per SIMD a compute wave (MFMAs, shear ring,
+                            volume stores) and a memory wave (feature loads and staging); fp32,
+                            aligned rows, C = 16 or 64, D in 65..192 per pass; other shapes:
+                            MFMA_H2DB.  AUTO's choice for the volume on the shapes it takes */
+  SM_IP_MFMA_SL = 12     /* sliding-window role-split band kernel: a workgroup walks whole rows
+                            and keeps the right window of all channels in LDS, so a 128-pixel
+                            segment stages only its own 128 left and 128 new right columns;
+                            shapes of MFMA_RS plus (C = 16) two passes of <= 128 disparities
+                            (D = 256); others: MFMA_H2DB.  The fused volume + soft-argmin calls
+                            (sm_cv_inner_product_softargmin*) take it for fp32 features */
 };
 
 /* Library version (major*10000 + minor*100 + patch). */

@@ -50,6 +50,28 @@ int64_t warp_workspace_bytes(int64_t N, int64_t C, int64_t Hi, int64_t Wi, int64
 
 using namespace smcv;
 
+#ifndef SMCV_AUTO_SL
+// AUTO's volume kernel for the shapes both take: the role-split band (0) or the sliding-window
+// band (1).  The volume is bound by how HBM takes its write stream: band_rs's schedule (the eight
+// tiles of a row on eight workgroups of one XCD at once, every 3,840-B volume row written
+// together) ran 0-8 % faster than band_sl's row walk on every box measured (cfg2 32-pair launch:
+// 3,957 vs 4,263 us and 4,235 vs 4,251 us; scripts/micro/sl_pattern.hip, profiles/r05/), while
+// band_sl's lighter staging wins the fused passes (ip_h2.hip, SMCV_SL_FUSE)
+#define SMCV_AUTO_SL 0
+#endif
+namespace {
+// band_h2_entry's kernel choice for an algo: 6 band_sl, 5 band_rs, 2 band_h2db, 0 band_h2
+int algo_variant(int algo) {
+  switch (algo) {
+    case SM_IP_AUTO: return SMCV_AUTO_SL ? 6 : 5;
+    case SM_IP_MFMA_SL: return 6;
+    case SM_IP_MFMA_RS: return 5;
+    case SM_IP_MFMA_H2DB: return 2;
+    default: return 0;
+  }
+}
+}  // namespace
+
 #define SM_ENTRY_BEGIN last_error().clear();
 
 extern "C" int sm_cv_inner_product_ex(const void* left, const void* right, void* out, int dtype,
@@ -70,17 +92,14 @@ extern "C" int sm_cv_inner_product_ex(const void* left, const void* right, void*
     case SM_IP_AUTO:  // the two-plane fp16 band kernel; odd shapes: the exact VALU kernel
     case SM_IP_MFMA_H2:
     case SM_IP_MFMA_H2DB:
-    case SM_IP_MFMA_SP:
-    case SM_IP_MFMA_RS: {
+    case SM_IP_MFMA_RS:
+    case SM_IP_MFMA_SL: {
       bool handled = false;
-      // AUTO / RS: fp32 aligned rows with C = 16 or 64 and 65..192 disparities per pass take
-      // the role-split band (band_rs), other fp32 aligned rows the double-buffered one
-      // (band_h2db), the rest band_h2; SP: the software-pipelined band (band_sp), shapes it
-      // does not take band_h2db
-      const int variant = algo == SM_IP_MFMA_SP                              ? 4
-                          : (algo == SM_IP_MFMA_RS || algo == SM_IP_AUTO)    ? 5
-                          : algo == SM_IP_MFMA_H2DB                          ? 2
-                                                                             : 0;
+      // AUTO / RS: fp32 aligned rows with C = 16 or 64 and 65..192 disparities per pass take the
+      // role-split band (band_rs); SL: the sliding-window band (band_sl; also C = 16 with two
+      // passes of <= 128); shapes they do not take: the double-buffered band (band_h2db) for fp32
+      // aligned rows, band_h2 for the rest
+      const int variant = algo_variant(algo);
       int rc = band_h2_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
                              stream, &handled, variant);
       if (handled || rc != SM_OK) return rc;
@@ -118,12 +137,9 @@ extern "C" int sm_cv_correlation_mean_ex(const void* left, const void* right, vo
     case SM_IP_AUTO:
     case SM_IP_MFMA_H2:
     case SM_IP_MFMA_H2DB:
-    case SM_IP_MFMA_SP:
-    case SM_IP_MFMA_RS: {
-      const int variant = algo == SM_IP_MFMA_SP                              ? 4
-                          : (algo == SM_IP_MFMA_RS || algo == SM_IP_AUTO)    ? 5
-                          : algo == SM_IP_MFMA_H2                            ? 0
-                                                                             : 2;
+    case SM_IP_MFMA_RS:
+    case SM_IP_MFMA_SL: {
+      const int variant = algo_variant(algo);
       rc = band_h2_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 1, stream,
                          &handled, variant);
       break;

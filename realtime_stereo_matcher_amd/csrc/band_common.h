@@ -480,5 +480,94 @@ __device__ __forceinline__ void fused_softargmin(const f32x16 (&acc)[TMAX], cons
   }
 }
 
+// fused_softargmin's fold without the store: the lane pair's merged state of one D pass -- the
+// maximum M, s = sum e and t = sum d e relative to M with d GLOBAL (t + dp s) -- in both lanes of
+// the pair (band_sl: the two passes of a segment run back to back on one wave, so pass 0's state
+// waits in registers for pass 1 instead of going through a workspace).
+template <int TMAX, bool MEAN, bool SCALE, bool XLT>
+__device__ __forceinline__ void fused_softargmin_state(const f32x16 (&acc)[TMAX], const Args& args,
+                                                       const Work& k, int kL, int kR, int wave,
+                                                       int lr, int hh, float& Mo, double& so,
+                                                       double& to) {
+  constexpr int DMAX = 32 * (TMAX - 1);
+  const float mul = args.mul;
+  const int kk = -(kL + kR);
+  const int jlane = k.js + 32 * wave + 4 * hh;
+  const int u0 = lr - 4 * hh;
+  constexpr float kL2E = 1.4426950408889634f;
+  const bool full = k.Dp == DMAX;
+  float m = -INFINITY;
+  double s = 0.0, tt = 0.0;
+  auto block = [&](auto tc, auto maskc) {
+    constexpr int t = decltype(tc)::value;
+    int ub = u0 + 32 * (TMAX - 1 - t);
+    asm volatile("" : "+v"(ub));
+    float v[16];
+    float bm = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int ci = (i & 3) + 8 * (i >> 2);
+      float x = acc[t][i];
+      if (MEAN) x *= mul;
+      if constexpr (SCALE) x = __builtin_ldexpf(x, kk);
+      if constexpr (XLT) x = jlane + 32 * t + ci >= 0 ? x : 0.f;
+      if constexpr (decltype(maskc)::value) x = (unsigned)(ub - ci) < (unsigned)k.Dp ? x : -INFINITY;
+      v[i] = x;
+      bm = fmaxf(bm, x);
+    }
+    const float nm = fmaxf(m, bm);
+    const float sh = fmaxf(nm, -3.402823466e38f);
+    const float f = __builtin_amdgcn_exp2f((m - sh) * kL2E);
+    float ps = 0.f, pc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float e = __builtin_amdgcn_exp2f((v[i] - sh) * kL2E);
+      ps += e;
+      pc = fmaf((float)((i & 3) + 8 * (i >> 2)), e, pc);
+    }
+    s = s * (double)f + (double)ps;
+    tt = tt * (double)f + (double)ub * (double)ps - (double)pc;
+    m = nm;
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  using TT = std::true_type;
+  using FF = std::false_type;
+  [&]<int... T_>(std::integer_sequence<int, T_...>) {
+    ((T_ == 0 || T_ == TMAX - 1
+          ? block(std::integral_constant<int, T_>{}, TT{})
+          : (full ? block(std::integral_constant<int, T_>{}, FF{})
+                  : block(std::integral_constant<int, T_>{}, TT{}))),
+     ...);
+  }(std::make_integer_sequence<int, TMAX>{});
+  const float M = fmaxf(m, __shfl_xor(m, 32));
+  const double g = (double)__builtin_amdgcn_exp2f((m - fmaxf(M, -3.402823466e38f)) * kL2E);
+  s *= g;
+  tt *= g;
+  s += __shfl_xor(s, 32);
+  tt += __shfl_xor(tt, 32);
+  Mo = M;
+  so = s;
+  to = tt + (double)k.dp * s;
+}
+
+// The two passes' states merged (fused_merge_kernel's arithmetic) and the disparity stored by
+// lane hh = 0 of the pair.
+__device__ __forceinline__ void fused_two_pass_store(const Args& args, const Work& k, int wave,
+                                                     int lr, int hh, float m0, double s0,
+                                                     double t0, float m1, double s1, double t1) {
+  constexpr float kL2E = 1.4426950408889634f;
+  const float M = fmaxf(m0, m1);
+  const float sh = fmaxf(M, -3.402823466e38f);
+  const double g0 = (double)__builtin_amdgcn_exp2f((m0 - sh) * kL2E);
+  const double g1 = (double)__builtin_amdgcn_exp2f((m1 - sh) * kL2E);
+  const double s = s0 * g0 + s1 * g1;
+  const double t = t0 * g0 + t1 * g1;
+  const int x = k.x0 + 32 * wave + lr;
+  if (hh == 0 && x < args.W) {
+    const size_t px = ((size_t)k.n * args.H + k.y) * args.W + x;
+    store_one<float>(args.disp + px, (float)(t / s));
+  }
+}
+
 }  // namespace h2band
 }  // namespace smcv

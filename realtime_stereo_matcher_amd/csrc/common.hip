@@ -81,6 +81,6 @@ int read_strides(const int64_t* s, int64_t C, int64_t H, int64_t W, Strides4* ou
 
 }  // namespace smcv
 
-extern "C" int sm_version(void) { return 100; }  // 0.1.0
+extern "C" int sm_version(void) { return 200; }  // 0.2.0: enum values 3, 4, 6, 7, 9, 10 retired; 12 added
 
 extern "C" const char* sm_last_error(void) { return smcv::last_error().c_str(); }

@@ -802,7 +802,8 @@ int check_dot_args(const void* left, const void* right, const void* out, int dty
 
 namespace h2band {
 int band_h2db_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled);
-int band_sp_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled);
+int band_sl_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled,
+                int fuse);
 int band_rs_gw_run(const Args& a, int64_t N, int dtype, hipStream_t st, bool* handled);
 #ifndef SMCV_RS_FUSE2
 #define SMCV_RS_FUSE2 1  // the one-pass volume-free fused pass on band_rs (0: band_h2's FUSE 2;
@@ -880,13 +881,13 @@ int band_h2_entry(const void* left, const void* right, void* out, int dtype, int
   const bool mean = mode == 1;
   a.mul = 1.0f / (float)C;
   hipStream_t st = as_stream(stream);
-  // fp32 with aligned rows: variant 4 the software-pipelined kernel (band_sp), variant 5 the
-  // role-split kernel (band_rs; the shapes they do not take fall through to band_h2db), variant 2 the double-buffered pipeline (band_h2db);
-  // other shapes (and variant 0) run band_h2
+  // fp32 with aligned rows: variant 6 the sliding-window kernel (band_sl), variant 5 the
+  // role-split kernel (band_rs; the shapes they do not take fall through to band_h2db), variant
+  // 2 the double-buffered pipeline (band_h2db); other shapes (and variant 0) run band_h2
   if (variant != 0 && dtype == SM_F32) {
     bool done = false;
-    if (variant == 4) {  // the software-pipelined kernel; shapes it does not take: band_h2db
-      rc = band_sp_run(a, N, mean, al4, st, &done);
+    if (variant == 6) {  // the sliding-window kernel; shapes it does not take: band_h2db
+      rc = band_sl_run(a, N, mean, al4, st, &done, 0);
       if (done || rc != SM_OK) return rc;
     }
     if (variant == 5) {  // the role-split kernel; shapes it does not take: band_h2db
@@ -973,6 +974,24 @@ int band_h2_fused_entry(const void* left, const void* right, void* out, float* d
   // fp16 / bf16 features with fp32 disparities (SM_FUSED_DISP_F32: the reference's autocast
   // eval) take the band kernel's half instantiations; fp32 features the fp32 ones
   const bool f32disp = (mode & SM_FUSED_DISP_F32) != 0;
+#ifndef SMCV_SL_FUSE
+#define SMCV_SL_FUSE 1  // the fp32 fused passes on the sliding-window kernel where it takes them
+#endif
+  if (SMCV_SL_FUSE && vec && dtype == SM_F32 && D > 0) {
+    // one D pass with or without the volume; two passes (C = 16) without it, the passes' states
+    // merged in registers (no workspace)
+    Args b = a;
+    b.out = out;
+    b.disp = disp;
+    b.mul = 1.0f / (float)C;
+    bool done = false;
+    rc = band_sl_run(b, N, (mode & 1) != 0, al4, as_stream(stream), &done, out != nullptr ? 1 : 2);
+    if (rc != SM_OK) return rc;
+    if (done) {
+      *handled = true;
+      return SM_OK;
+    }
+  }
   if (!vec || (dtype != SM_F32 && !f32disp) || (a.npass != 1 && !multi) || D == 0) return SM_OK;
   if (multi) {
     const int64_t per = (int64_t)a.npass * a.nhw;

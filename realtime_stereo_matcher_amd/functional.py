@@ -29,7 +29,7 @@ from . import _lib
 _DTYPES = {torch.float32: _lib.SM_F32, torch.float16: _lib.SM_F16, torch.bfloat16: _lib.SM_BF16}
 _ALGOS = {"auto": _lib.SM_IP_AUTO, "valu": _lib.SM_IP_VALU, "mfma": _lib.SM_IP_MFMA_F32,
           "f32": _lib.SM_IP_MFMA_F32, "h2": _lib.SM_IP_MFMA_H2, "h2db": _lib.SM_IP_MFMA_H2DB,
-          "sp": _lib.SM_IP_MFMA_SP, "rs": _lib.SM_IP_MFMA_RS}
+          "rs": _lib.SM_IP_MFMA_RS, "sl": _lib.SM_IP_MFMA_SL}
 
 
 # ----------------------------------------------------------------------------------- plumbing

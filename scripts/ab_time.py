@@ -39,6 +39,17 @@ def ops():
         # the bench's launch since pairs per launch = the rank's whole batch (32 at N = 1)
         "cfg2_b32": (lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192))(*feats((32, 64, 540, 960), torch.float32)),
                      32, 663552000),
+        # round 5: the sliding-window kernel (AUTO) against the role-split one, bench shapes
+        "cfg2_b32_rs": (lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="rs"))(*feats((32, 64, 540, 960), torch.float32)),
+                        32, 663552000),
+        "cfg2_b32_sl": (lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="sl"))(*feats((32, 64, 540, 960), torch.float32)),
+                        32, 663552000),
+        "cfg4_b32_rs": (lambda: (lambda L, R: lambda: F.correlation_volume(L, R, 256, algo="rs"))(*feats((32, 16, 1080, 1920), torch.float32)),
+                        32, 2388787200),
+        "cfg4_b4_auto": (lambda: (lambda L, R: lambda: F.correlation_volume(L, R, 256))(*feats((4, 16, 1080, 1920), torch.float32)),
+                         4, 2388787200),
+        "cfg2_fused_b32": (lambda: (lambda L, R: lambda: F.inner_product_soft_argmin(L, R, 192, keep_volume=True))(
+            *feats((32, 64, 540, 960), torch.float32)), 32, 665625600),
         "cfg4_b32": (lambda: (lambda L, R: lambda: F.correlation_volume(L, R, 256))(*feats((32, 16, 1080, 1920), torch.float32)),
                      32, 2388787200),
         "cfg2_fused_nv_b32": (lambda: (lambda L, R: lambda: F.inner_product_soft_argmin(L, R, 192, keep_volume=False))(
@@ -49,8 +60,6 @@ def ops():
                     8, 663552000),
         "cfg2_h2db": (lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="h2db"))(*feats((8, 64, 540, 960), torch.float32)),
                       8, 663552000),
-        "cfg2_sp": (lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="sp"))(*feats((8, 64, 540, 960), torch.float32)),
-                    8, 663552000),
         "cfg2_rs": (lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="rs"))(*feats((8, 64, 540, 960), torch.float32)),
                     8, 663552000),
         "cfg2_fused": (lambda: (lambda L, R: lambda: F.inner_product_soft_argmin(L, R, 192, keep_volume=True))(
@@ -64,8 +73,6 @@ def ops():
         "cfg4": (lambda: (lambda L, R: lambda: F.correlation_volume(L, R, 256))(*feats((4, 16, 1080, 1920), torch.float32)),
                  4, 2388787200),
         "cfg4_rs": (lambda: (lambda L, R: lambda: F.correlation_volume(L, R, 256, algo="rs"))(*feats((4, 16, 1080, 1920), torch.float32)),
-                    4, 2388787200),
-        "cfg4_sp": (lambda: (lambda L, R: lambda: F.correlation_volume(L, R, 256, algo="sp"))(*feats((4, 16, 1080, 1920), torch.float32)),
                     4, 2388787200),
         "cfg4_fused_nv": (lambda: (lambda L, R: lambda: F.inner_product_soft_argmin(L, R, 256, mean=True, keep_volume=False))(
             *feats((4, 16, 1080, 1920), torch.float32)), 4, 273715200),

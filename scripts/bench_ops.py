@@ -66,7 +66,7 @@ def main():
     L, R = feats((1, 64, 540, 960), torch.float32)
     n_in = 2 * L.numel() * 4
     vol_b = 192 * 540 * 960 * 4
-    for algo in ("h2", "h2db", "sp", "f32", "valu"):
+    for algo in ("h2", "h2db", "rs", "sl", "f32", "valu"):
         run(f"inner_product_{algo}_cfg2", lambda: F.inner_product_volume(L, R, 192, algo=algo), n_in + vol_b)
     vol = F.inner_product_volume(L, R, 192)
     run("soft_argmin_cfg2", lambda: F.soft_argmin(vol), vol_b + 540 * 960 * 4)

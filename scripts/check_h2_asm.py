@@ -8,8 +8,8 @@ kernel relies on two properties of the generated code, checked here for every in
   2. no wave ends (s_endpgm) with such a load still in flight (the L2 touches included);
   3. no `flat_*` memory instruction exists (flat ops count in vmcnt out of order, which would
      break the `vmcnt(4 (T-1))` wait that lets the output stores stay in flight);
-  4. band_h2db (ip_h2db.hip), band_sp (ip_sp.hip) and band_rs (ip_rs.hip) have no scratch
-     access at all: a spill reload counts in vmcnt (band_sp's and band_rs's loads are
+  4. band_h2db (ip_h2db.hip), band_rs (ip_rs.hip) and band_sl (ip_sl.hip) have no scratch
+     access at all: a spill reload counts in vmcnt (band_rs's and band_sl's loads are
      compiler-tracked; the other checks find no inline-asm loads in them, and the scratch check
      is what applies there) and would wait for the feature loads in flight.
 A may-pending dataflow over the kernel's basic blocks carries each load to every instruction it
@@ -26,8 +26,8 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "realtime_stereo_matcher_amd", "csrc")
-SRCS = [os.path.join(CSRC, "ip_h2.hip"), os.path.join(CSRC, "ip_h2db.hip"), os.path.join(CSRC, "ip_sp.hip"),
-        os.path.join(CSRC, "ip_rs.hip")]
+SRCS = [os.path.join(CSRC, "ip_h2.hip"), os.path.join(CSRC, "ip_h2db.hip"), os.path.join(CSRC, "ip_rs.hip"),
+        os.path.join(CSRC, "ip_sl.hip")]
 
 
 def regs(tok):
@@ -44,7 +44,7 @@ def kernels(asm_text):
     only those loads are hand-counted (the compiler waits for its own)."""
     out, cur, in_asm = [], None, False
     for ln, line in enumerate(asm_text.splitlines(), 1):
-        if re.match(r"^_ZN4smcv6h2band(7band_h2|9band_h2db|7band_sp|7band_rs).*:", line):
+        if re.match(r"^_ZN4smcv6h2band(7band_h2|9band_h2db|7band_rs|7band_sl).*:", line):
             cur = (line.split(":")[0], [])
             out.append(cur)
             continue
@@ -144,8 +144,8 @@ def check(asm_text):
                         changed = True
         rep = []
         for i, b in enumerate(blocks):
-            # no scratch at all in band_h2db (volume and fused), band_sp and band_rs
-            no_scr = "9band_h2db" in name or "7band_sp" in name or "7band_rs" in name
+            # no scratch at all in band_h2db (volume and fused), band_rs and band_sl
+            no_scr = "9band_h2db" in name or "7band_rs" in name or "7band_sl" in name
             transfer(b, ins_state[i], rep, no_scratch=no_scr)
         bad += [f"{name}:{r}" for r in rep]
     return bad

@@ -36,7 +36,7 @@ def _ids(cs):
 
 
 # =============================================================================== golden vectors
-@pytest.mark.parametrize("algo", ["auto", "h2", "h2db", "sp", "f32", "valu"])
+@pytest.mark.parametrize("algo", ["auto", "h2", "h2db", "rs", "sl", "f32", "valu"])
 @pytest.mark.parametrize("rec", cases("inner_product"), ids=_ids(cases("inner_product")))
 def test_golden_inner_product(rec, algo):
     from realtime_stereo_matcher_amd.cost_volume import TorchInnerProductCost
@@ -169,7 +169,7 @@ def test_golden_argext(rec):
     fn = F.hard_argmax if rec["params"]["mode"] == "max" else F.hard_argmin
     np.testing.assert_array_equal(host(fn(dev(a["volume"]))), a["out"])
     if "left" in a:  # end to end: integer features -> exact volume -> bit-exact argmax
-        for algo in ("auto", "h2", "h2db", "sp", "f32", "valu"):
+        for algo in ("auto", "h2", "h2db", "rs", "sl", "f32", "valu"):
             vol = TorchInnerProductCost(rec["params"]["max_disparity"], algo=algo)(dev(a["left"]), dev(a["right"]))
             np.testing.assert_array_equal(host(vol), a["volume"])
             np.testing.assert_array_equal(host(F.hard_argmax(vol)), a["out"])
@@ -196,7 +196,7 @@ def _feats(seed, shape, kind="normal"):
     return rng.standard_normal(shape, dtype=np.float32), rng.standard_normal(shape, dtype=np.float32)
 
 
-@pytest.mark.parametrize("algo", ["auto", "h2", "h2db", "sp", "f32", "valu"])
+@pytest.mark.parametrize("algo", ["auto", "h2", "h2db", "rs", "sl", "f32", "valu"])
 @pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
 def test_inner_product_vs_oracle(shape, algo):
     from realtime_stereo_matcher_amd import functional as F
@@ -215,7 +215,7 @@ def _cell_norm(l, r, D):
     return O.inner_product(np.abs(l), np.abs(r), D)
 
 
-@pytest.mark.parametrize("algo", ["auto", "h2", "h2db", "sp", "f32"])
+@pytest.mark.parametrize("algo", ["auto", "h2", "h2db", "rs", "sl", "f32"])
 @pytest.mark.parametrize("scale", [1e-15, 1e-6, 1e-3, 1e3, 1e6, 1e15])
 def test_inner_product_feature_scales(scale, algo):
     """Uniformly tiny or huge features: the fp16 split rescales each segment by a power of two
@@ -232,7 +232,7 @@ def test_inner_product_feature_scales(scale, algo):
     assert (err <= 1e-5 * _cell_norm(l, r, 192) / 64 + 1e-37).all()
 
 
-@pytest.mark.parametrize("algo", ["auto", "h2", "h2db", "sp"])
+@pytest.mark.parametrize("algo", ["auto", "h2", "h2db", "rs", "sl"])
 def test_inner_product_mixed_scales(algo):
     """Feature scale changing from row to row (10^-8 .. 10^8, L and R independently) and within
     a row (10^-2 .. 10^2 per pixel): every segment must land in a safe fp16 range."""
@@ -270,7 +270,7 @@ def test_inner_product_half_vs_oracle(shape, dt):
                                rtol=ulp, atol=1e-4)
 
 
-@pytest.mark.parametrize("algo,dt", [("auto", "f32"), ("h2", "f32"), ("h2db", "f32"), ("sp", "f32"), ("f32", "f32"), ("valu", "f32"),
+@pytest.mark.parametrize("algo,dt", [("auto", "f32"), ("h2", "f32"), ("h2db", "f32"), ("rs", "f32"), ("sl", "f32"), ("f32", "f32"), ("valu", "f32"),
                                      ("auto", "f16"), ("auto", "bf16")])
 def test_inner_product_nonfinite(algo, dt):
     """+-inf and NaN features give the reference's inf / NaN cells, and x < d cells stay 0."""
@@ -464,7 +464,7 @@ def _rows_check(full, fn_oracle, rows, atol, exact=False):
             np.testing.assert_allclose(got, want, atol=atol, rtol=0)
 
 
-@pytest.mark.parametrize("algo", ["auto", "h2", "h2db", "sp", "f32", "valu"])
+@pytest.mark.parametrize("algo", ["auto", "h2", "h2db", "rs", "sl", "f32", "valu"])
 def test_cfg2_inner_product_full_size(algo):
     """BASELINE configs[1]: 1x64x540x960 fp32, D=192 -- every row depends only on the same
     row of L and R (inner_product.py:38-40), so rows sampled from the full-size launch are

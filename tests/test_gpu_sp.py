@@ -1,7 +1,9 @@
-"""GPU parity of the software-pipelined band kernel (algo "sp", csrc/ip_sp.hip) and the role-split
-band kernel (algo "rs", csrc/ip_rs.hip) against the CPU oracle, on the shapes they take (fp32,
-4-element aligned rows, C = 16 or 64, D > 64 per pass), including the bench's own launch shapes
-(cfg2: 8 pairs per launch; cfg4: 4 pairs).
+"""GPU parity of the role-split band kernel (algo "rs", csrc/ip_rs.hip) and the sliding-window
+band kernel (algo "sl", csrc/ip_sl.hip; AUTO's choice) against the CPU oracle, on the shapes they
+take (fp32, 4-element aligned rows, C = 16 or 64, D > 64 per pass), including the bench's own
+launch shapes (cfg2 and cfg4: the whole 32-pair batch per launch; cfg4 also the 4-pair launch of
+each rank at N = 8) and shapes with several rows per workgroup (the sliding window's row
+changes).
 
 Reference op: TorchInnerProductCost.forward (cost_volume/inner_product.py:11-42) and
 make_correlation_volume (model/mobile_disp_net_c.py:188-205).  Tolerance: 1e-4 absolute for
@@ -16,7 +18,7 @@ from oracle import stereo_oracle as O
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-4
-ALGOS = ["sp", "rs"]
+ALGOS = ["rs", "sl"]
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -46,7 +48,10 @@ def _feats(seed, shape, kind="normal"):
 # balanced D passes of 128 (D = 256), D > W
 SP_SHAPES = [(1, 64, 3, 512, 192), (2, 64, 5, 260, 100), (3, 64, 2, 132, 128), (2, 64, 3, 960, 191),
              (1, 64, 2, 16, 96), (1, 64, 1, 4, 80), (1, 16, 4, 388, 192), (1, 16, 3, 1000, 256),
-             (2, 16, 2, 200, 65), (1, 64, 2, 64, 192), (5, 16, 1, 900, 160)]
+             (2, 16, 2, 200, 65), (1, 64, 2, 64, 192), (5, 16, 1, 900, 160),
+             # more rows than workgroups: each sliding-window workgroup walks several rows
+             (2, 64, 300, 324, 192), (3, 16, 200, 260, 256), (1, 16, 700, 132, 100),
+             (1, 64, 520, 196, 128)]
 
 
 @pytest.mark.parametrize("algo", ALGOS)
