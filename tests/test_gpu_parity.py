@@ -617,7 +617,12 @@ def test_groupwise_band_nonfinite():
 
 FUSED_SHAPES = [(1, 64, 3, 512, 192), (2, 20, 3, 260, 100), (1, 33, 2, 132, 31), (1, 16, 2, 64, 64),
                 (1, 8, 3, 100, 24), (1, 7, 2, 36, 40), (1, 16, 2, 64, 256), (1, 5, 2, 33, 9),
-                (1, 64, 2, 958, 192), (2, 20, 2, 259, 100)]
+                (1, 64, 2, 958, 192), (2, 20, 2, 259, 100),
+                # C = 16 one channel step, both band geometries (the fused C = 16
+                # instantiations of the sliding-window / role-split kernels), and more rows than
+                # workgroups (the sliding window's row changes), C = 16 and 64
+                (2, 16, 3, 260, 100), (1, 16, 2, 388, 192), (1, 16, 300, 196, 160),
+                (2, 64, 150, 260, 192)]
 
 
 @pytest.mark.parametrize("mean", [False, True])
@@ -646,11 +651,13 @@ def test_fused_soft_argmin(shape, mean):
 
 
 @pytest.mark.parametrize("mean", [False, True])
-@pytest.mark.parametrize("shape", [(1, 16, 2, 320, 256), (2, 24, 2, 257, 300), (1, 8, 3, 64, 200)], ids=str)
+@pytest.mark.parametrize("shape", [(1, 16, 2, 320, 256), (2, 24, 2, 257, 300), (1, 8, 3, 64, 200),
+                                   (1, 16, 300, 260, 256), (2, 16, 3, 132, 200)], ids=str)
 def test_fused_soft_argmin_multipass(shape, mean):
-    """Volume-free fused pass for D > 192 (MobileDispNetC's D = 256): per-pass partial softmax
-    states in a workspace, merged by a second kernel; the disparity is the fp64 soft-argmin of
-    the volume op's volume within 1e-4."""
+    """Volume-free fused pass for D > 192 (MobileDispNetC's D = 256): C = 16 takes the
+    sliding-window kernel's two passes with the states merged in registers; other shapes per-pass
+    partial softmax states in a workspace, merged by a second kernel.  The disparity is the fp64
+    soft-argmin of the volume op's volume within 1e-4."""
     from realtime_stereo_matcher_amd import _lib
     from realtime_stereo_matcher_amd import functional as F
 
@@ -669,7 +676,7 @@ def test_fused_soft_argmin_multipass(shape, mean):
 
 def test_cfg4_fused_volume_free_full_res():
     """BASELINE configs[3] shape (1x16x1080x1920, correlation D = 256) through the volume-free
-    fused path (two passes + merge): the disparity matches the two-kernel pipeline's (volume,
+    fused path (band_sl: two passes per segment, merged in registers): the disparity matches the two-kernel pipeline's (volume,
     then soft-argmin) within 1e-4 everywhere, and sampled rows match the fp64 soft-argmin of
     the volume."""
     from realtime_stereo_matcher_amd import functional as F
@@ -706,10 +713,10 @@ def test_fused_soft_argmin_nonfinite_and_empty():
 @pytest.mark.parametrize("mean", [False, True])
 @pytest.mark.parametrize("kind", ["nonfinite", "tiny"])
 def test_fused_volume_free_multipass_exact_segments(kind, mean):
-    """D = 256 without the volume (two passes + merge) on segments that take the band kernel's
-    exact fp32 path: +-inf / NaN features, or a feature scale the fp16 split cannot reach
-    (max |L| ~ 2^-91).  Each pass must leave its partial softmax state in the workspace (NaN
-    carried as NaN), so the merged disparity equals the two-kernel pipeline's."""
+    """D = 256 without the volume (band_sl's two passes merged in registers) on segments that
+    take the band kernel's exact fp32 path: +-inf / NaN features, or a feature scale the fp16
+    split cannot reach (max |L| ~ 2^-91).  NaN is carried as NaN, so the merged disparity equals
+    the two-kernel pipeline's."""
     from realtime_stereo_matcher_amd import functional as F
 
     l, r = _feats(24 if kind == "nonfinite" else 25, (1, 16, 3, 320))
