@@ -39,11 +39,16 @@ enum sm_status {
 enum sm_argext_mode { SM_ARGMIN = 0, SM_ARGMAX = 1 };
 /* sm_cv_inner_product_softargmin*: mode = 0 (sum) or 1 (mean), optionally OR'd with */
 enum sm_fused_flags {
-  SM_FUSED_DISP_F32 = 2 /* the disparity is float32 whatever the feature dtype: the reference's
-                           autocast eval, where the volume keeps the fp16 / bf16 feature dtype and
-                           F.softmax + torch.sum run in fp32 (evaluate_stereo.py:48,
-                           mobile_disp_net_c.py:208-220); fp16 / bf16 features then take the
-                           fused band kernel too */
+  SM_FUSED_DISP_F32 = 2, /* the disparity is float32 whatever the feature dtype: the reference's
+                            autocast eval, where the volume keeps the fp16 / bf16 feature dtype and
+                            F.softmax + torch.sum run in fp32 (evaluate_stereo.py:48,
+                            mobile_disp_net_c.py:208-220); fp16 / bf16 features then take the
+                            fused band kernel too, which regresses each cell rounded to the
+                            feature dtype -- the volume the reference's two calls regress */
+  SM_FUSED_EXACT_ACC = 4 /* with SM_FUSED_DISP_F32 and fp16 / bf16 features: regress the fp32
+                            accumulators of the exact products instead (no rounding to the
+                            feature dtype; shapes the fused kernel does not take still regress
+                            the rounded volume) */
 };
 enum sm_regress_flags {         /* bit flags */
   SM_REGRESS_SOFTMAX = 0,      /* softmax over D inside (mobile_disp_net_c.py:208-220) */
@@ -235,7 +240,8 @@ int sm_warp_by_flow_ws(const void* image, const void* flow, void* out, int dtype
  * w2 (32,16,4,3,3) b2 (32), w3 (16,32,2,3,3) b3 (16), w4 (16) b4 (1).
  * workspace: device scratch of at least sm_v4_volume_workspace_bytes(N, H, W) bytes (per-pixel
  * layer-1 tables + packed MFMA weights); the library allocates nothing.
- * Arithmetic: layer 1 fp32; layers 2-3 bf16 MFMA over hi/lo-split fp32 operands (3 products). */
+ * Arithmetic: layer 1 fp32; layers 2-3 fp16 MFMA over per-layer power-of-two scaled, hi/lo-split
+ * fp32 operands (3 products, fp32 accumulation). */
 int64_t sm_v4_volume_workspace_bytes(int64_t N, int64_t H, int64_t W);
 int sm_v4_volume(const void* featL, const void* featR, void* out, int dtype,
                  int64_t N, int64_t C, int64_t H, int64_t W, int64_t D,

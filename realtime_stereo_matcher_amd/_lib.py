@@ -15,6 +15,7 @@ SM_OK, SM_EINVAL, SM_EDTYPE, SM_ELAUNCH, SM_EUNSUPPORTED = 0, -1, -2, -3, -4
 SM_ARGMIN, SM_ARGMAX = 0, 1
 SM_REGRESS_SOFTMAX, SM_REGRESS_PRESOFTMAXED, SM_REGRESS_OUT_F32 = 0, 1, 2
 SM_FUSED_DISP_F32 = 2
+SM_FUSED_EXACT_ACC = 4
 SM_IP_AUTO, SM_IP_VALU, SM_IP_MFMA_F32, SM_IP_MFMA_H2, SM_IP_MFMA_H2DB, SM_IP_MFMA_RS, SM_IP_MFMA_SL = 0, 1, 2, 5, 8, 11, 12
 
 _p = ctypes.c_void_p

@@ -181,8 +181,9 @@ int fused_softargmin(const void* left, const void* right, void* out_volume, void
                      int dtype, int64_t N, int64_t C, int64_t H, int64_t W, int64_t D,
                      const int64_t* l_strides, const int64_t* r_strides, int mode,
                      void* workspace, int64_t ws_bytes, void* stream) {
-  if ((mode & ~(1 | SM_FUSED_DISP_F32)) != 0)
-    return fail(SM_EINVAL, "mode must be 0 (sum) or 1 (mean), optionally | SM_FUSED_DISP_F32");
+  if ((mode & ~(1 | SM_FUSED_DISP_F32 | SM_FUSED_EXACT_ACC)) != 0)
+    return fail(SM_EINVAL,
+                "mode must be 0 (sum) or 1 (mean), optionally | SM_FUSED_DISP_F32 | SM_FUSED_EXACT_ACC");
   const bool f32disp = (mode & SM_FUSED_DISP_F32) != 0;
   if (!valid_dtype(dtype)) return fail(SM_EDTYPE, "unsupported dtype code");
   if (ws_bytes < 0) return fail(SM_EINVAL, "negative workspace size");

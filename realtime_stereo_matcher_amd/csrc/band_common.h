@@ -1,5 +1,5 @@
 // Helpers shared by the band cost-volume kernels (ip_h2.hip: band_h2; ip_h2db.hip: band_h2db;
-// ip_sp.hip: band_sp):
+// ip_rs.hip: band_rs; ip_sl.hip: band_sl):
 // operand typedefs, the plane swizzle, the work decomposition, LDS accessors, the hand-counted
 // feature loads and their vmcnt wait, the output stores and the fp32 two-plane split.
 #pragma once
@@ -62,6 +62,7 @@ struct Args {
   Strides4 ls, rs;
   int tiles, npass, pw, nwork;
   float mul;  // MEAN: 1 / (channels averaged)
+  int round;  // fused pass of fp16 / bf16 features: regress the cells rounded to the feature dtype
   // volume-free fused kernel with npass > 1: each pass's partial soft-argmin state per pixel
   // (max, sum e, sum d e relative to that max), merged by fused_merge_kernel
   double* ws_s;
@@ -272,7 +273,7 @@ __device__ __forceinline__ void split_quad(const float (&x)[8], float sc, uint4&
 // exponent e with x = f 2^e, f in [0.5, 1) (x > 0 finite)
 __device__ __forceinline__ int exp_of(float x) { return __builtin_amdgcn_frexp_expf(x); }
 
-// The persistent grid's schedule (band_h2, band_h2db, band_sp).  Workgroups b and b+8 share an
+// The persistent grid's schedule (band_h2, band_h2db, band_rs).  Workgroups b and b+8 share an
 // XCD, and each XCD group walks a contiguous range of row segments, so neighbouring segments of
 // a row run on one XCD at the same time and share its L2 for the right window.  Item i of a
 // workgroup is segment j = gi + (i / npass) gsz of its group's range, pass i % npass: the D
@@ -383,50 +384,39 @@ __device__ __forceinline__ void slow_softargmin_f32(const Args& args, const Work
   }
 }
 
-// Soft-argmin straight from a wave's band accumulators (the fused pass, f-1).  Lane (lr, hh)
-// holds, for pixel x0 + 32 wave + lr, the cells of local disparity dl = 32 (T-1-t) + u - c_i
-// (block t, element i, u = lr - 4 hh), and the lane pair (lr, 0), (lr, 1) holds every d of the
-// pixel exactly once.  One pass, block by block (every accumulator element read once): the
-// block's maximum, the running sums rescaled when it grows, the block's exps summed in fp32 and
-// carried into fp64.  Cells outside 0 <= dl < Dp enter as -inf (e = 0); only the first and the
-// last block can hold such cells when Dp == DMAX.  No NaN / inf flags: a NaN cell makes its e
-// NaN, a +inf maximum makes (inf - inf) NaN, an all -inf pixel gives 0 / 0 -- torch's NaN each
-// time.  The shift max(m, -FLT_MAX) keeps exp2 finite-argument when no cell is finite yet.  The
-// pair merges by one shuffle; lane hh = 0 stores the disparity (one pass) or the pass's partial
-// state (several D passes, args.ws_m).  SCALE multiplies back by 2^-(kL+kR); XLT forces the
-// cells x < d (R pad rows) to 0, as the volume has them.  WS: the partial-state form exists
-// (several D passes); without it only the disparity store is compiled.
-template <int TMAX, bool MEAN, bool SCALE, bool XLT, bool WS = true>
-__device__ __forceinline__ void fused_softargmin(const f32x16 (&acc)[TMAX], const Args& args,
-                                                 const Work& k, int kL, int kR, int wave, int lr,
-                                                 int hh) {
+// One block of the fused soft-argmin fold (shared by every fused path, so a fold split between
+// waves performs the same arithmetic in the same order as one wave's): lane (lr, hh) holds, for
+// pixel x0 + 32 wave + lr, the cells of local disparity dl = 32 (T-1-t) + u - c_i (block t,
+// element i, u = lr - 4 hh).  The block's maximum, the running sums (m, s = sum e, tt = sum dl e,
+// relative to m) rescaled when it grows, the block's exps summed in fp32 and carried into fp64.
+// Cells outside 0 <= dl < Dp enter as -inf (e = 0): the first and the last block always, the
+// middle ones when Dp < DMAX.  No NaN / inf flags: a NaN cell makes its e NaN, a +inf maximum
+// makes (inf - inf) NaN, an all -inf pixel gives 0 / 0 -- torch's NaN each time.  The shift
+// max(m, -FLT_MAX) keeps exp2 finite-argument when no cell is finite yet.  SCALE multiplies back
+// by 2^-(kL+kR); XLT forces the cells x < d (R pad rows) to 0, as the volume has them; RT (not
+// float): the cell rounded to RT first.
+template <int TMAX, bool MEAN, bool SCALE, bool XLT, typename RT, int t>
+__device__ __forceinline__ void fold_block(const f32x16& blk, const Args& args, const Work& k,
+                                           int kL, int kR, int wave, int lr, int hh, float& m,
+                                           double& s, double& tt) {
   constexpr int DMAX = 32 * (TMAX - 1);
+  constexpr float kL2E = 1.4426950408889634f;
   const float mul = args.mul;
   const int kk = -(kL + kR);
   const int jlane = k.js + 32 * wave + 4 * hh;
-  const int u0 = lr - 4 * hh;
-  auto value = [&](int t, int i) {
-    const int ci = (i & 3) + 8 * (i >> 2);
-    float val = acc[t][i];
-    if (MEAN) val *= mul;
-    if constexpr (SCALE) val = __builtin_ldexpf(val, kk);
-    if constexpr (XLT) val = jlane + 32 * t + ci >= 0 ? val : 0.f;
-    return val;
-  };
-  constexpr float kL2E = 1.4426950408889634f;
-  const bool full = k.Dp == DMAX;
-  float m = -INFINITY;
-  double s = 0.0, tt = 0.0;
-  auto block = [&](auto tc, auto maskc) {
-    constexpr int t = decltype(tc)::value;
-    int ub = u0 + 32 * (TMAX - 1 - t);  // dl = ub - c_i; opaque per block (not hoisted)
+  auto body = [&](auto maskc) __attribute__((always_inline)) {
+    int ub = lr - 4 * hh + 32 * (TMAX - 1 - t);  // dl = ub - c_i; opaque per block (not hoisted)
     asm volatile("" : "+v"(ub));
     float v[16];
     float bm = -INFINITY;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int ci = (i & 3) + 8 * (i >> 2);
-      float x = value(t, i);
+      float x = blk[i];
+      if (MEAN) x *= mul;
+      if constexpr (SCALE) x = __builtin_ldexpf(x, kk);
+      if constexpr (XLT) x = jlane + 32 * t + ci >= 0 ? x : 0.f;
+      if constexpr (!std::is_same<RT, float>::value) x = (float)(RT)x;
       if constexpr (decltype(maskc)::value) x = (unsigned)(ub - ci) < (unsigned)k.Dp ? x : -INFINITY;
       v[i] = x;
       bm = fmaxf(bm, x);
@@ -448,22 +438,49 @@ __device__ __forceinline__ void fused_softargmin(const f32x16 (&acc)[TMAX], cons
   };
   // the first and the last block always straddle the band's ends; the middle ones only when
   // Dp < DMAX (a uniform branch: the common full-D item runs them unmasked)
-  using TT = std::true_type;
-  using FF = std::false_type;
-  [&]<int... T_>(std::integer_sequence<int, T_...>) {
-    ((T_ == 0 || T_ == TMAX - 1
-          ? block(std::integral_constant<int, T_>{}, TT{})
-          : (full ? block(std::integral_constant<int, T_>{}, FF{})
-                  : block(std::integral_constant<int, T_>{}, TT{}))),
-     ...);
-  }(std::make_integer_sequence<int, TMAX>{});
-  // the other row half of the pixel
-  const float M = fmaxf(m, __shfl_xor(m, 32));
+  if constexpr (t == 0 || t == TMAX - 1)
+    body(std::true_type{});
+  else if (k.Dp == DMAX)
+    body(std::false_type{});
+  else
+    body(std::true_type{});
+}
+
+// Blocks [B0, B1) of a wave's accumulators folded into (m, s, tt).
+template <int TMAX, bool MEAN, bool SCALE, bool XLT, typename RT, int B0, int B1>
+__device__ __forceinline__ void fold_blocks(const f32x16* blk, const Args& args, const Work& k,
+                                            int kL, int kR, int wave, int lr, int hh, float& m,
+                                            double& s, double& tt) {
+  [&]<int... T_>(std::integer_sequence<int, T_...>) __attribute__((always_inline)) {
+    (fold_block<TMAX, MEAN, SCALE, XLT, RT, B0 + T_>(blk[T_], args, k, kL, kR, wave, lr, hh, m, s, tt), ...);
+  }(std::make_integer_sequence<int, B1 - B0>{});
+}
+
+// The lane pair's merge: (lr, 0) and (lr, 1) hold the two row halves of the pixel; after it both
+// hold M and the sums relative to M.
+__device__ __forceinline__ void fold_pair_merge(float m, double& s, double& tt, float& M) {
+  constexpr float kL2E = 1.4426950408889634f;
+  M = fmaxf(m, __shfl_xor(m, 32));
   const double g = (double)__builtin_amdgcn_exp2f((m - fmaxf(M, -3.402823466e38f)) * kL2E);
   s *= g;
   tt *= g;
   s += __shfl_xor(s, 32);
   tt += __shfl_xor(tt, 32);
+}
+
+// Soft-argmin straight from a wave's band accumulators (the fused pass, f-1): every block folded
+// (fold_block), the pair merged by one shuffle; lane hh = 0 stores the disparity (one pass) or the
+// pass's partial state (several D passes, args.ws_m).  WS: the partial-state form exists (several
+// D passes); without it only the disparity store is compiled.
+template <int TMAX, bool MEAN, bool SCALE, bool XLT, bool WS = true, typename RT = float>
+__device__ __forceinline__ void fused_softargmin(const f32x16 (&acc)[TMAX], const Args& args,
+                                                 const Work& k, int kL, int kR, int wave, int lr,
+                                                 int hh) {
+  float m = -INFINITY;
+  double s = 0.0, tt = 0.0;
+  fold_blocks<TMAX, MEAN, SCALE, XLT, RT, 0, TMAX>(acc, args, k, kL, kR, wave, lr, hh, m, s, tt);
+  float M;
+  fold_pair_merge(m, s, tt, M);
   const int x = k.x0 + 32 * wave + lr;
   if (hh == 0 && x < args.W) {
     const size_t px = ((size_t)k.n * args.H + k.y) * args.W + x;
@@ -484,68 +501,15 @@ __device__ __forceinline__ void fused_softargmin(const f32x16 (&acc)[TMAX], cons
 // maximum M, s = sum e and t = sum d e relative to M with d GLOBAL (t + dp s) -- in both lanes of
 // the pair (band_sl: the two passes of a segment run back to back on one wave, so pass 0's state
 // waits in registers for pass 1 instead of going through a workspace).
-template <int TMAX, bool MEAN, bool SCALE, bool XLT>
+template <int TMAX, bool MEAN, bool SCALE, bool XLT, typename RT = float>
 __device__ __forceinline__ void fused_softargmin_state(const f32x16 (&acc)[TMAX], const Args& args,
                                                        const Work& k, int kL, int kR, int wave,
                                                        int lr, int hh, float& Mo, double& so,
                                                        double& to) {
-  constexpr int DMAX = 32 * (TMAX - 1);
-  const float mul = args.mul;
-  const int kk = -(kL + kR);
-  const int jlane = k.js + 32 * wave + 4 * hh;
-  const int u0 = lr - 4 * hh;
-  constexpr float kL2E = 1.4426950408889634f;
-  const bool full = k.Dp == DMAX;
   float m = -INFINITY;
   double s = 0.0, tt = 0.0;
-  auto block = [&](auto tc, auto maskc) {
-    constexpr int t = decltype(tc)::value;
-    int ub = u0 + 32 * (TMAX - 1 - t);
-    asm volatile("" : "+v"(ub));
-    float v[16];
-    float bm = -INFINITY;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int ci = (i & 3) + 8 * (i >> 2);
-      float x = acc[t][i];
-      if (MEAN) x *= mul;
-      if constexpr (SCALE) x = __builtin_ldexpf(x, kk);
-      if constexpr (XLT) x = jlane + 32 * t + ci >= 0 ? x : 0.f;
-      if constexpr (decltype(maskc)::value) x = (unsigned)(ub - ci) < (unsigned)k.Dp ? x : -INFINITY;
-      v[i] = x;
-      bm = fmaxf(bm, x);
-    }
-    const float nm = fmaxf(m, bm);
-    const float sh = fmaxf(nm, -3.402823466e38f);
-    const float f = __builtin_amdgcn_exp2f((m - sh) * kL2E);
-    float ps = 0.f, pc = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float e = __builtin_amdgcn_exp2f((v[i] - sh) * kL2E);
-      ps += e;
-      pc = fmaf((float)((i & 3) + 8 * (i >> 2)), e, pc);
-    }
-    s = s * (double)f + (double)ps;
-    tt = tt * (double)f + (double)ub * (double)ps - (double)pc;
-    m = nm;
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  using TT = std::true_type;
-  using FF = std::false_type;
-  [&]<int... T_>(std::integer_sequence<int, T_...>) {
-    ((T_ == 0 || T_ == TMAX - 1
-          ? block(std::integral_constant<int, T_>{}, TT{})
-          : (full ? block(std::integral_constant<int, T_>{}, FF{})
-                  : block(std::integral_constant<int, T_>{}, TT{}))),
-     ...);
-  }(std::make_integer_sequence<int, TMAX>{});
-  const float M = fmaxf(m, __shfl_xor(m, 32));
-  const double g = (double)__builtin_amdgcn_exp2f((m - fmaxf(M, -3.402823466e38f)) * kL2E);
-  s *= g;
-  tt *= g;
-  s += __shfl_xor(s, 32);
-  tt += __shfl_xor(tt, 32);
-  Mo = M;
+  fold_blocks<TMAX, MEAN, SCALE, XLT, RT, 0, TMAX>(acc, args, k, kL, kR, wave, lr, hh, m, s, tt);
+  fold_pair_merge(m, s, tt, Mo);
   so = s;
   to = tt + (double)k.dp * s;
 }

@@ -81,6 +81,7 @@ int read_strides(const int64_t* s, int64_t C, int64_t H, int64_t W, Strides4* ou
 
 }  // namespace smcv
 
-extern "C" int sm_version(void) { return 200; }  // 0.2.0: enum values 3, 4, 6, 7, 9, 10 retired; 12 added
+extern "C" int sm_version(void) { return 201; }  // 0.2.1: enum values 3, 4, 6, 7, 9, 10 retired; 12 added; SM_FUSED_DISP_F32 rounds the
+                                                   // cells (SM_FUSED_EXACT_ACC: the old form)
 
 extern "C" const char* sm_last_error(void) { return smcv::last_error().c_str(); }

@@ -336,9 +336,18 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
   // Fused soft-argmin straight from the accumulators (fused_softargmin, band_common.h; shared
   // with band_h2db's FUSE 1).  No ring, no LDS: the volume-free kernel never shears.
   // (fp16 / bf16 features: exact products, no scale -- SCALE is false for them)
+  // args.round (fp16 / bf16 features under autocast, the default): the fold sees each cell
+  // rounded to the feature dtype, as the reference's volume holds it
   auto fuse_regs = [&](const Work& k, auto scale, auto xlt) {
-    fused_softargmin<TMAX, MEAN, decltype(scale)::value, decltype(xlt)::value>(acc, args, k, kL, kR,
-                                                                               wave, lr, hh);
+    constexpr bool SC = decltype(scale)::value, XL = decltype(xlt)::value;
+    if constexpr (std::is_same<T, float>::value) {
+      fused_softargmin<TMAX, MEAN, SC, XL>(acc, args, k, kL, kR, wave, lr, hh);
+    } else {
+      if (args.round)
+        fused_softargmin<TMAX, MEAN, SC, XL, true, T>(acc, args, k, kL, kR, wave, lr, hh);
+      else
+        fused_softargmin<TMAX, MEAN, SC, XL>(acc, args, k, kL, kR, wave, lr, hh);
+    }
   };
 
   // SCALE: multiply back by 2^-(kL+kR); XLT: the segment has cells x < d (R pad rows), forced
@@ -804,6 +813,7 @@ namespace h2band {
 int band_h2db_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled);
 int band_sl_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled,
                 int fuse);
+int band_sl_half_run(const Args& a, int64_t N, bool mean, int dtype, hipStream_t st, bool* handled);
 int band_rs_gw_run(const Args& a, int64_t N, int dtype, hipStream_t st, bool* handled);
 #ifndef SMCV_RS_FUSE2
 #define SMCV_RS_FUSE2 1  // the one-pass volume-free fused pass on band_rs (0: band_h2's FUSE 2;
@@ -857,6 +867,7 @@ int h2_prepare(const void* left, const void* right, const void* out, int dtype, 
   a->pw = (int)pw;
   a->nwork = 0;
   a->mul = 1.0f;
+  a->round = 0;
   a->ws_s = a->ws_t = nullptr;
   a->ws_m = nullptr;
   a->nhw = N * H * W;
@@ -974,6 +985,9 @@ int band_h2_fused_entry(const void* left, const void* right, void* out, float* d
   // fp16 / bf16 features with fp32 disparities (SM_FUSED_DISP_F32: the reference's autocast
   // eval) take the band kernel's half instantiations; fp32 features the fp32 ones
   const bool f32disp = (mode & SM_FUSED_DISP_F32) != 0;
+  // fp16 / bf16 features: the fold regresses the cells rounded to the feature dtype (the
+  // reference's autocast result) unless SM_FUSED_EXACT_ACC asks for the fp32 accumulators
+  a.round = dtype != SM_F32 && (mode & SM_FUSED_EXACT_ACC) == 0;
 #ifndef SMCV_SL_FUSE
 #define SMCV_SL_FUSE 1  // the fp32 fused passes on the sliding-window kernel where it takes them
 #endif
@@ -1006,6 +1020,14 @@ int band_h2_fused_entry(const void* left, const void* right, void* out, float* d
   const bool mean = (mode & 1) != 0;
   hipStream_t st = as_stream(stream);
   if (dtype != SM_F32) {  // exact products of the half features, one MFMA per block and step
+#ifndef SMCV_SL_HALF
+#define SMCV_SL_HALF 0  // the volume-free pass of fp16 / bf16 features on the sliding-window kernel
+#endif
+    if (SMCV_SL_HALF && out == nullptr && al4) {
+      bool done = false;
+      rc = band_sl_half_run(a, N, mean, dtype, st, &done);
+      if (done || rc != SM_OK) return rc;
+    }
     auto go_half = [&](auto tag) {
       using T = typename decltype(tag)::type;
       return by_tmax(a.pw, [&](auto tm) {

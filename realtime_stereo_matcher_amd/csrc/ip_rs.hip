@@ -35,7 +35,7 @@
 //   * no inline asm names an accumulator register class, so the compiler keeps the accumulators
 //     in ordinary VGPRs: both roles share one 256-register budget (2 waves per SIMD).
 // Pad pixels, the restart on a scale change, the exact slow path for non-finite segments and
-// the x < d forcing are band_sp's (see ip_sp.hip).
+// the x < d forcing come from band_sp (round 4; scripts/experimental/ip_sp.hip).
 #include "band_common.h"
 
 #ifndef SMCV_RS_ABLATE
@@ -134,7 +134,7 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
 #ifdef SMCV_RS_STAMPS
   unsigned long long st_[10] = {}, t_ = __builtin_amdgcn_s_memtime();
 #endif
-  constexpr int SB = isC ? 0 : 5;  // this role's first stamp slot
+  [[maybe_unused]] constexpr int SB = isC ? 0 : 5;  // this role's first stamp slot
   const int lane = tid & 63;
   const int lr = lane & 31;
   const int hh = lane >> 5;
@@ -741,9 +741,11 @@ int band_rs_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t 
     constexpr int NS = NK == 1 ? 2 : SMCV_RS_SETS;
     auto f = [&](auto fc) {
       constexpr int FU = decltype(fc)::value;
-      if constexpr (FU == 1 && NK == 1 && TM == 7)  // (excluded above for the mean)
+      if constexpr (FU == 1 && NK == 1 && TM == 7) {
+        // (the mean is excluded above: its compute wave would spill; never a silent sum)
+        if (mean) return fail(SM_EINVAL, "band_rs: unhandled fused mean shape");
         return launch_rs<false, TM, NK, NS, FU>(a, N, st);
-      else
+      } else
         return mean ? launch_rs<true, TM, NK, NS, FU>(a, N, st)
                     : launch_rs<false, TM, NK, NS, FU>(a, N, st);
     };

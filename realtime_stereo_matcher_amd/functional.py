@@ -22,6 +22,8 @@ Reference operators mirrored (babiking/realtime_stereo_matcher):
 from __future__ import annotations
 
 import numpy as np
+import threading
+
 import torch
 
 from . import _lib
@@ -145,7 +147,29 @@ def _autocast_fp32(*ts):
     The engine follows: under autocast these ops return fp32 (one rounding, from fp64 / fp32
     arithmetic), never the volume's reduced dtype.
     """
+    ov = getattr(_decided, "f32", None)
+    if ov is not None:  # the body of a torch.ops.stereocv op: the decision made at trace time
+        return ov
     return any(t.dtype in _HALF for t in ts) and torch.is_autocast_enabled(ts[0].device.type)
+
+
+_decided = threading.local()
+
+
+class _F32Decided:
+    """Inside a torch.ops.stereocv op (library.py) the fp32-output decision is an op argument
+    taken when the graph was traced, not the autocast state at run time: a compiled graph may run
+    its ops after the compiler removed the autocast regions."""
+
+    def __init__(self, value):
+        self.value = bool(value)
+
+    def __enter__(self):
+        self.prev = getattr(_decided, "f32", None)
+        _decided.f32 = self.value
+
+    def __exit__(self, *exc):
+        _decided.f32 = self.prev
 
 
 # ----------------------------------------------------------------------------- a-1, a-6, a-2
@@ -178,7 +202,7 @@ def correlation_volume(l_fmap, r_fmap, max_disp, algo="auto"):
     if algo not in _ALGOS:
         raise ValueError(f"algo must be one of {sorted(_ALGOS)}")
     if _traced():
-        return _ops().correlation_volume(l_fmap, r_fmap, int(max_disp))
+        return _ops().correlation_volume(l_fmap, r_fmap, int(max_disp), algo)
     left, right, dev, code = _pair(l_fmap, r_fmap, "correlation_volume")
     D = _disp(max_disp, "correlation_volume")
     n, c, h, w = left.shape
@@ -196,24 +220,39 @@ def correlation_volume(l_fmap, r_fmap, max_disp, algo="auto"):
     return _run(fn, left, right)
 
 
-def inner_product_soft_argmin(left, right, max_disparity, mean=False, keep_volume=True):
+def inner_product_soft_argmin(left, right, max_disparity, mean=False, keep_volume=True,
+                              exact_accumulators=False):
     """Cost volume + soft-argmin in one kernel pass.
 
     The inner-product volume (cost_volume/inner_product.py:11-42; ``mean=True``: the
     correlation volume of model/mobile_disp_net_c.py:188-205) and its disparity regression
     sum_d d * softmax_d(volume) (model/mobile_disp_net_c.py:208-220, = the inline soft-argmin of
     model/mobile_stereo_net.py:144-147).  Returns ``(volume, disparity)``: the (N,D,H,W) volume
-    (``None`` with ``keep_volume=False``: it is then never written) and the (N,1,H,W) disparity,
-    both in the feature dtype.  fp32 features (W >= 4) run one fused band kernel for D <= 192;
-    without the volume also for D > 192 (passes of <= 192 disparities whose partial softmax
-    states a second kernel merges, in a workspace allocated here); other shapes run the volume
-    and the regression kernels back to back.
+    (``None`` with ``keep_volume=False``: it is then never written) and the (N,1,H,W) disparity.
+
+    Precision, per the reference's two calls:
+    - fp32 features: the volume and the disparity are fp32; the disparity is the soft-argmin of
+      exactly the volume returned (bit-identical between ``keep_volume`` True and False).
+    - fp16 / bf16 features outside autocast: both in the feature dtype.
+    - fp16 / bf16 features under ``torch.autocast`` (the reference's default eval,
+      evaluate_stereo.py:48): the volume keeps the feature dtype and the disparity is fp32, the
+      soft-argmin of the volume's cells as rounded to the feature dtype -- what the reference's
+      ``disparity_regression(corr_volume)`` regresses -- on every shape.  ``exact_accumulators=
+      True`` regresses the fp32 accumulators of the exact products instead (no rounding), on the
+      shapes the fused kernel takes (4-element aligned rows; D <= 192 with the volume kept);
+      the other shapes regress the rounded volume either way.
+
+    fp32 features (W >= 4) run one fused band kernel for D <= 192 and, without the volume, for
+    C = 16 and D <= 256 (two D passes per segment merged in registers) or other D > 192 (passes
+    of <= 192 disparities whose partial softmax states a second kernel merges, in a workspace
+    allocated here); other shapes run the volume and the regression kernels back to back.
     """
     if _traced():
+        f32, ex = _autocast_fp32(left), bool(exact_accumulators)
         if keep_volume:
-            return _ops().inner_product_soft_argmin(left, right, int(max_disparity), bool(mean))
+            return _ops().inner_product_soft_argmin(left, right, int(max_disparity), bool(mean), f32, ex)
         return None, _ops().inner_product_soft_argmin_novolume(left, right, int(max_disparity),
-                                                               bool(mean))
+                                                               bool(mean), f32, ex)
     left, right, dev, code = _pair(left, right, "inner_product_soft_argmin")
     D = _disp(max_disparity, "inner_product_soft_argmin")
     n, c, h, w = left.shape
@@ -224,6 +263,8 @@ def inner_product_soft_argmin(left, right, max_disparity, mean=False, keep_volum
     f32disp = _autocast_fp32(left)
     if f32disp:
         mode |= _lib.SM_FUSED_DISP_F32
+        if exact_accumulators:
+            mode |= _lib.SM_FUSED_EXACT_ACC
 
     def call(vol, disp):
         lib = _lib.load()
@@ -434,7 +475,7 @@ def soft_argmin(volume, keepdim=True):
     The output has the volume's dtype; under torch autocast an fp16 / bf16 volume gives fp32
     (the reference's autocast F.softmax + torch.sum)."""
     if _traced():
-        out = _ops().soft_argmin(volume)
+        out = _ops().soft_argmin(volume, _autocast_fp32(volume))
         return out.unsqueeze(1) if keepdim else out
     out = _regress(volume, _lib.SM_REGRESS_SOFTMAX, "soft_argmin")
     return out.unsqueeze(1) if keepdim else out
@@ -444,7 +485,7 @@ def regression_presoftmax(prob):
     """sum_d d * prob[:, d] over an already-softmaxed (N,D,H,W) volume -> (N,H,W) (fp32 under
     autocast for an fp16 / bf16 input, the reference's autocast torch.sum)."""
     if _traced():
-        return _ops().regression_presoftmax(prob)
+        return _ops().regression_presoftmax(prob, _autocast_fp32(prob))
     return _regress(prob, _lib.SM_REGRESS_PRESOFTMAXED, "regression_presoftmax")
 
 
@@ -493,7 +534,7 @@ def warp_by_flow_map(image, flow):
     if not isinstance(image, torch.Tensor) or not isinstance(flow, torch.Tensor):
         raise TypeError("warp_by_flow_map: image and flow must be tensors")
     if _traced():
-        return _ops().warp_by_flow_map(image, flow)
+        return _ops().warp_by_flow_map(image, flow, _autocast_fp32(image, flow))
     if flow.dim() != 4:
         raise ValueError(f"warp_by_flow_map: expected a 4-D flow map, got {tuple(flow.shape)}")
     n, c, h, w = flow.shape

@@ -75,12 +75,13 @@ def _inner_product_fake(left, right, max_disparity, algo):
     return _empty((n, max_disparity, h, w), left)
 
 
-def _correlation(left: torch.Tensor, right: torch.Tensor, max_disp: int) -> torch.Tensor:
+def _correlation(left: torch.Tensor, right: torch.Tensor, max_disp: int,
+                 algo: str = "auto") -> torch.Tensor:
     with _Inside():
-        return F.correlation_volume(left, right, max_disp)
+        return F.correlation_volume(left, right, max_disp, algo=algo)
 
 
-def _correlation_fake(left, right, max_disp):
+def _correlation_fake(left, right, max_disp, algo="auto"):
     n, _, h, w = left.shape
     return _empty((n, max_disp, h, w), left)
 
@@ -136,29 +137,30 @@ def _difference_fake(left, right, max_disp):
     return _empty((n, c, max_disp, h, w), left)
 
 
-def _regress_dtype(volume):
-    # the autocast rule of functional._regress: fp32 from a half volume under autocast
-    return torch.float32 if F._autocast_fp32(volume) else volume.dtype
+def _regress_dtype(volume, f32):
+    # the autocast rule of functional._regress, decided when the graph was traced (f32: an
+    # fp16 / bf16 volume under autocast gives fp32)
+    return torch.float32 if f32 else volume.dtype
 
 
-def _soft_argmin(volume: torch.Tensor) -> torch.Tensor:
-    with _Inside():
+def _soft_argmin(volume: torch.Tensor, f32: bool = False) -> torch.Tensor:
+    with _Inside(), F._F32Decided(f32):
         return F.soft_argmin(volume, keepdim=False)
 
 
-def _soft_argmin_fake(volume):
+def _soft_argmin_fake(volume, f32=False):
     n, _, h, w = volume.shape
-    return _empty((n, h, w), volume, _regress_dtype(volume))
+    return _empty((n, h, w), volume, _regress_dtype(volume, f32))
 
 
-def _presoftmax(prob: torch.Tensor) -> torch.Tensor:
-    with _Inside():
+def _presoftmax(prob: torch.Tensor, f32: bool = False) -> torch.Tensor:
+    with _Inside(), F._F32Decided(f32):
         return F.regression_presoftmax(prob)
 
 
-def _presoftmax_fake(prob):
+def _presoftmax_fake(prob, f32=False):
     n, _, h, w = prob.shape
-    return _empty((n, h, w), prob, _regress_dtype(prob))
+    return _empty((n, h, w), prob, _regress_dtype(prob, f32))
 
 
 def _argext_fake(volume):
@@ -176,45 +178,47 @@ def _hard_argmax(volume: torch.Tensor) -> torch.Tensor:
         return F.hard_argmax(volume)
 
 
-def _fused(left: torch.Tensor, right: torch.Tensor, max_disparity: int,
-           mean: bool) -> tuple[torch.Tensor, torch.Tensor]:
-    with _Inside():
-        return F.inner_product_soft_argmin(left, right, max_disparity, mean=mean, keep_volume=True)
+def _fused(left: torch.Tensor, right: torch.Tensor, max_disparity: int, mean: bool,
+           f32: bool = False, exact: bool = False) -> tuple[torch.Tensor, torch.Tensor]:
+    with _Inside(), F._F32Decided(f32):
+        return F.inner_product_soft_argmin(left, right, max_disparity, mean=mean, keep_volume=True,
+                                           exact_accumulators=exact)
 
 
-def _fused_disp_dtype(left):
-    # autocast with half features: the two-kernel path whose soft-argmin returns fp32
-    return torch.float32 if F._autocast_fp32(left) else left.dtype
+def _fused_disp_dtype(left, f32):
+    # autocast with half features (decided when the graph was traced): fp32 disparities
+    return torch.float32 if f32 else left.dtype
 
 
-def _fused_fake(left, right, max_disparity, mean):
+def _fused_fake(left, right, max_disparity, mean, f32=False, exact=False):
     n, _, h, w = left.shape
     return (_empty((n, max_disparity, h, w), left),
-            _empty((n, 1, h, w), left, _fused_disp_dtype(left)))
+            _empty((n, 1, h, w), left, _fused_disp_dtype(left, f32)))
 
 
-def _fused_novolume(left: torch.Tensor, right: torch.Tensor, max_disparity: int,
-                    mean: bool) -> torch.Tensor:
-    with _Inside():
+def _fused_novolume(left: torch.Tensor, right: torch.Tensor, max_disparity: int, mean: bool,
+                    f32: bool = False, exact: bool = False) -> torch.Tensor:
+    with _Inside(), F._F32Decided(f32):
         return F.inner_product_soft_argmin(left, right, max_disparity, mean=mean,
-                                           keep_volume=False)[1]
+                                           keep_volume=False, exact_accumulators=exact)[1]
 
 
-def _fused_novolume_fake(left, right, max_disparity, mean):
+def _fused_novolume_fake(left, right, max_disparity, mean, f32=False, exact=False):
     n, _, h, w = left.shape
-    return _empty((n, 1, h, w), left, _fused_disp_dtype(left))
+    return _empty((n, 1, h, w), left, _fused_disp_dtype(left, f32))
 
 
-def _warp(image: torch.Tensor, flow: torch.Tensor) -> torch.Tensor:
-    with _Inside():
+def _warp(image: torch.Tensor, flow: torch.Tensor, f32: bool = False) -> torch.Tensor:
+    with _Inside(), F._F32Decided(f32):
         return F.warp_by_flow_map(image, flow)
 
 
-def _warp_fake(image, flow):
+def _warp_fake(image, flow, f32=False):
     # the output dtype rule of functional.warp_by_flow_map: fp32 under autocast (grid_sample is
-    # an autocast fp32 op), else the shared image / flow dtype
+    # an autocast fp32 op; decided when the graph was traced), else the image dtype (fp32 for an
+    # fp32 image)
     n, _, h, w = flow.shape
-    odt = torch.float32 if F._autocast_fp32(image, flow) else image.dtype
+    odt = torch.float32 if f32 else image.dtype
     return _empty((n, image.shape[1], h, w), image, odt)
 
 

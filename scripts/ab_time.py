@@ -31,6 +31,11 @@ def _warp_nows(img, flow):
     return out
 
 
+def _autocast(f):
+    with torch.autocast("cuda", dtype=torch.float16):
+        return f()
+
+
 def ops():
     return {
         # name: (setup -> callable, pairs per launch, algorithmic bytes per pair)
@@ -50,6 +55,10 @@ def ops():
                          4, 2388787200),
         "cfg2_fused_b32": (lambda: (lambda L, R: lambda: F.inner_product_soft_argmin(L, R, 192, keep_volume=True))(
             *feats((32, 64, 540, 960), torch.float32)), 32, 665625600),
+        "cfg2_fused_nv_f16_b32": (lambda: (lambda L, R: lambda: _autocast(lambda: F.inner_product_soft_argmin(L, R, 192, keep_volume=False)))(
+            *feats((32, 64, 540, 960), torch.float16)), 32, 134784000),
+        "cfg4_fused_nv_f16_b32": (lambda: (lambda L, R: lambda: _autocast(lambda: F.inner_product_soft_argmin(L, R, 256, mean=True, keep_volume=False)))(
+            *feats((32, 16, 1080, 1920), torch.float16)), 32, 74649600 + 8294400),
         "cfg4_b32": (lambda: (lambda L, R: lambda: F.correlation_volume(L, R, 256))(*feats((32, 16, 1080, 1920), torch.float32)),
                      32, 2388787200),
         "cfg2_fused_nv_b32": (lambda: (lambda L, R: lambda: F.inner_product_soft_argmin(L, R, 192, keep_volume=False))(

@@ -17,7 +17,18 @@ from oracle import stereo_oracle as O
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-4
-DISP_RTOL = 4e-6  # fused disparity vs the fp64 soft-argmin of the exact volume (see below)
+
+
+def _fp32_bar(ln, rn, D, mean, exact_disp):
+    """The per-pixel bar for a disparity regressed from fp32 sums of exact products: max(1e-4,
+    2 x torch fp32's own deviation from the fp64 pipeline on the same pixels) -- the stated form
+    the full-size cfg2 test uses (fp32 rounding of the cells is amplified by sharp softmaxes at a
+    few pixels, for torch as for the kernel)."""
+    from oracle.torch_port import soft_argmin_eager, sweep_dot_volume
+
+    v32 = sweep_dot_volume(torch.from_numpy(ln), torch.from_numpy(rn), D, mean=mean)
+    dev32 = np.abs(soft_argmin_eager(v32).numpy().astype(np.float64) - exact_disp)
+    return np.maximum(TOL, 2.0 * dev32)
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -61,6 +72,9 @@ def test_presoftmax_regression_under_autocast():
 
 
 def test_fused_call_under_autocast_fp16_features():
+    """The reference's autocast result (disparity_regression of the fp16 corr_volume,
+    mobile_disp_net_c.py:191-192,217-219): the fused call regresses each cell rounded to fp16,
+    so its disparity is the soft-argmin of the fp16 volume it returns."""
     from realtime_stereo_matcher_amd import functional as F
 
     l = torch.randn(1, 32, 4, 128, device="cuda").half()
@@ -68,12 +82,16 @@ def test_fused_call_under_autocast_fp16_features():
     with torch.autocast("cuda", dtype=torch.float16):
         vol, disp = F.inner_product_soft_argmin(l, r, 48)
         none, disp2 = F.inner_product_soft_argmin(l, r, 48, keep_volume=False)
+        _, disp_x = F.inner_product_soft_argmin(l, r, 48, exact_accumulators=True)
     assert vol.dtype == torch.float16 and disp.dtype == torch.float32 and none is None
-    # the fused kernel regresses the fp32 accumulators of the exact products, not the volume
-    # rounded to fp16 (SM_FUSED_DISP_F32): compare with the soft-argmin of the exact volume
-    exact = O.inner_product(l.float().cpu().numpy(), r.float().cpu().numpy(), 48)
-    np.testing.assert_allclose(disp.cpu().numpy(), O.softargmin(exact), atol=TOL, rtol=DISP_RTOL)
-    np.testing.assert_allclose(disp2.cpu().numpy(), disp.cpu().numpy(), atol=1e-6, rtol=0)
+    np.testing.assert_allclose(disp.cpu().numpy(), O.softargmin(vol.float().cpu().numpy()),
+                               atol=TOL, rtol=0)
+    assert torch.equal(disp2, disp)  # the same fold with or without the volume
+    # opt-in: the fp32 accumulators of the exact products, against the fp64 pipeline
+    ln, rn = l.float().cpu().numpy(), r.float().cpu().numpy()
+    exact = O.softargmin(O.inner_product(ln, rn, 48))
+    err = np.abs(disp_x.cpu().numpy().astype(np.float64) - exact)
+    assert (err <= _fp32_bar(ln, rn, 48, False, exact)).all(), float(err.max())
 
 
 def test_warp_under_autocast_fp16_feature_map_fp32_flow():
@@ -120,33 +138,42 @@ def test_networks_run_under_autocast(v):
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("keep", [True, False])
 @pytest.mark.parametrize("shape,mean", [((1, 64, 4, 960, 192), False), ((2, 32, 3, 260, 100), False),
-                                        ((1, 16, 3, 512, 256), True), ((1, 64, 2, 128, 48), True)],
+                                        ((1, 16, 3, 512, 256), True), ((1, 64, 2, 128, 48), True),
+                                        ((1, 16, 2, 258, 100), False)],
                          ids=str)
 def test_fused_volume_softargmin_half_features_under_autocast(shape, mean, keep, dt):
-    """SURVEY §8f-1 at the reference's default precision (VERDICT r03 "missing 2"): fp16 / bf16
+    """SURVEY §8f-1 at the reference's default precision (VERDICT r04 "missing 3"): fp16 / bf16
     features under autocast take the fused band kernel (SM_FUSED_DISP_F32), whose soft-argmin
-    runs on the fp32 accumulators of the exact products: the disparity is fp32 and within 1e-4 of
-    the fp64 soft-argmin of the exact volume (the two-kernel path would regress the volume
-    rounded to the feature dtype, off by ~1e-3); the kept volume is the volume op's, bit for bit.
-    D = 256 volume-free runs two D passes and the merge kernel."""
+    regresses each cell rounded to the feature dtype, as the reference's two calls do
+    (mobile_disp_net_c.py:191-192,217-219 under evaluate_stereo.py:48).  The fp32 disparity is
+    within 1e-4, rtol 0, of the fp64 soft-argmin of the dtype-rounded volume (the engine's own
+    volume op: fp32 sums of the exact products, rounded once); the kept volume is that volume bit
+    for bit.  W % 4 != 0 (258) takes the two-kernel path, which regresses the same rounded
+    volume.  ``exact_accumulators=True`` regresses the fp32 accumulators instead: within the
+    stated fp32 bar of the exact fp64 pipeline.  D = 256 volume-free: two D passes + the merge."""
     from realtime_stereo_matcher_amd import functional as F
 
     n, c, h, w, D = shape
     rng = np.random.default_rng(hash(shape) % 1000)
     l = torch.from_numpy(rng.standard_normal((n, c, h, w), dtype=np.float32)).cuda().to(dt)
     r = torch.from_numpy(rng.standard_normal((n, c, h, w), dtype=np.float32)).cuda().to(dt)
-    ln, rn = l.float().cpu().numpy(), r.float().cpu().numpy()
-    exact = (O.correlation_mean if mean else O.inner_product)(ln, rn, D)
-    want = O.softargmin(exact)
     if keep and D > 192:
         pytest.skip("D > 192 with the volume kept is the two-kernel path by contract")
+    ref_vol = F.correlation_volume(l, r, D) if mean else F.inner_product_volume(l, r, D)
+    want = O.softargmin(ref_vol.float().cpu().numpy())  # the dtype-rounded volume, fp64 regression
     with torch.autocast("cuda", dtype=torch.float16):
         vol, disp = F.inner_product_soft_argmin(l, r, D, mean=mean, keep_volume=keep)
+        _, disp_x = F.inner_product_soft_argmin(l, r, D, mean=mean, keep_volume=keep,
+                                                exact_accumulators=True)
     assert disp.dtype == torch.float32 and disp.shape == (n, 1, h, w)
-    # fp32 sums of exact products vs the fp64 volume: cells differ by ~1e-6 relative, which the
-    # regression carries into the disparity (|d - disp| weighted): 1e-4 plus 4e-6 of disp
-    np.testing.assert_allclose(disp.cpu().numpy(), want, atol=TOL, rtol=DISP_RTOL)
+    np.testing.assert_allclose(disp.cpu().numpy(), want, atol=TOL, rtol=0)
     if keep:
         assert vol.dtype == dt
-        ref_vol = F.correlation_volume(l, r, D) if mean else F.inner_product_volume(l, r, D)
         assert torch.equal(vol, ref_vol)
+    ln, rn = l.float().cpu().numpy(), r.float().cpu().numpy()
+    exact = O.softargmin((O.correlation_mean if mean else O.inner_product)(ln, rn, D))
+    if w % 4 == 0:
+        err = np.abs(disp_x.cpu().numpy().astype(np.float64) - exact)
+        assert (err <= _fp32_bar(ln, rn, D, mean, exact)).all(), float(err.max())
+    else:  # not a fused shape: the rounded volume either way
+        np.testing.assert_allclose(disp_x.cpu().numpy(), want, atol=TOL, rtol=0)

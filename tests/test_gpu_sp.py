@@ -197,6 +197,24 @@ def test_sp_cfg4_bench_launch_shape(algo):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("algo", ALGOS)
+def test_sp_cfg4_rank_launch_at_n8(algo):
+    """The per-rank cfg4 launch at N = 8 (global batch 32 sharded over 8 GPUs: 4 pairs of
+    16x1080x1920 fp32, correlation D = 256, mobile_disp_net_c.py:365-367): rows of every pair
+    (first, middle, last, and the rows around each XCD range boundary of the schedule) against
+    the oracle."""
+    from realtime_stereo_matcher_amd import functional as F
+
+    g = torch.Generator(device="cuda").manual_seed(5)
+    L = torch.randn(4, 16, 1080, 1920, device="cuda", generator=g)
+    R = torch.randn(4, 16, 1080, 1920, device="cuda", generator=g)
+    vol = F.correlation_volume(L, R, 256, algo=algo)
+    torch.cuda.synchronize()
+    _check_rows(vol, L, R, 256, (0, 539, 540, 1079), mean=True)
+    del vol
+    torch.cuda.empty_cache()
+
+
 # groupwise volumes of 16-bit features on the role-split kernel ((N, G, H, W, D) fp32 output,
 # the ring in pixel-record layout): group steps of 16 / 32 / 64 channels, D = 68..192 (D < DMAX
 # takes the masked readout), ragged W, several pairs; exact products, so within 1e-4 of the

@@ -163,3 +163,33 @@ def test_jit_trace_fused_volume_regression(keep):
     want = want if isinstance(want, tuple) else (want,)
     for a, b in zip(got, want):
         torch.testing.assert_close(a, b, rtol=0, atol=0)
+
+
+@pytest.mark.gpu
+def test_autocast_decision_fixed_at_trace_time():
+    """the fp32-output choice of the regression / fused / warp ops under autocast is
+    an op argument taken when the graph is traced, so a graph traced under autocast returns what
+    its fake kernels promised even when it later runs with autocast off (as a compiler that
+    removed the autocast regions would run it)."""
+    from realtime_stereo_matcher_amd import functional as F
+
+    class Net(torch.nn.Module):
+        def forward(self, l, r, v, img, fl):
+            _, d = F.inner_product_soft_argmin(l, r, 96, keep_volume=False)
+            return F.soft_argmin(v), d, F.warp_by_flow_map(img, fl)
+
+    g = torch.Generator(device="cuda").manual_seed(9)
+    args = (torch.randn(1, 32, 4, 128, device="cuda", generator=g).half(),
+            torch.randn(1, 32, 4, 128, device="cuda", generator=g).half(),
+            torch.randn(1, 24, 4, 40, device="cuda", generator=g).half(),
+            torch.randn(1, 8, 4, 40, device="cuda", generator=g).half(),
+            torch.rand(1, 1, 4, 40, device="cuda", generator=g).half())
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.float16):
+        traced = torch.jit.trace(Net(), args)
+        want = Net()(*args)
+    assert all(t.dtype == torch.float32 for t in want)
+    with torch.no_grad():  # autocast off at run time
+        got = traced(*args)
+    for a, b in zip(got, want):
+        assert a.dtype == torch.float32
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
