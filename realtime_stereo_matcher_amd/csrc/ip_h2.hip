@@ -813,7 +813,6 @@ namespace h2band {
 int band_h2db_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled);
 int band_sl_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t st, bool* handled,
                 int fuse);
-int band_sl_half_run(const Args& a, int64_t N, bool mean, int dtype, hipStream_t st, bool* handled);
 int band_rs_gw_run(const Args& a, int64_t N, int dtype, hipStream_t st, bool* handled);
 #ifndef SMCV_RS_FUSE2
 #define SMCV_RS_FUSE2 1  // the one-pass volume-free fused pass on band_rs (0: band_h2's FUSE 2;
@@ -1020,14 +1019,6 @@ int band_h2_fused_entry(const void* left, const void* right, void* out, float* d
   const bool mean = (mode & 1) != 0;
   hipStream_t st = as_stream(stream);
   if (dtype != SM_F32) {  // exact products of the half features, one MFMA per block and step
-#ifndef SMCV_SL_HALF
-#define SMCV_SL_HALF 0  // the volume-free pass of fp16 / bf16 features on the sliding-window kernel
-#endif
-    if (SMCV_SL_HALF && out == nullptr && al4) {
-      bool done = false;
-      rc = band_sl_half_run(a, N, mean, dtype, st, &done);
-      if (done || rc != SM_OK) return rc;
-    }
     auto go_half = [&](auto tag) {
       using T = typename decltype(tag)::type;
       return by_tmax(a.pw, [&](auto tm) {

@@ -48,9 +48,6 @@
 #ifndef SMCV_SL_NTSTORE
 #define SMCV_SL_NTSTORE SMCV_NT_STORE  // volume stores non-temporal
 #endif
-#ifndef SMCV_SL_OFFLOAD
-#define SMCV_SL_OFFLOAD 0  // volume-free pass: the memory waves finish the soft-argmin fold (0: the
-#endif                     // compute waves fold everything, for A/B)
 #ifndef SMCV_SL_SETS
 #define SMCV_SL_SETS 4  // feature-load register sets (loads issued SETS - 1 steps ahead)
 #endif
@@ -65,35 +62,21 @@ constexpr int kKC = 16;                // channels per step (one 32x32x16 k-step
 constexpr int kSlot = 32 * 32 * 4;     // one shear chunk: 32 d x 32 x fp32
 constexpr int kBlk = 32 * 32;          // one 32-row block of one fp16 plane (16 channels)
 
-template <int TMAX, int NKS, int NP, int FUSE, int NPL = 2>
-struct Geo {  // NPL: fp16 planes per staged step (fp32 features: h and m; fp16 / bf16: one)
+template <int TMAX, int NKS, int NP, int FUSE>
+struct Geo {
   static constexpr int DMAX = 32 * (TMAX - 1);
   // R ring blocks per channel step: the window (4 + NP DMAX/32 blocks at most), plus four slack
   // blocks when one step must stage the next segment's columns while its own window is in use
   static constexpr int NB = NKS >= 2 ? (TMAX - 1) + 4 : NP * (TMAX - 1) + 8;
   static constexpr int RPL = NB * kBlk;          // one plane (h or m) of one channel step
-  static constexpr int RSTEP = NPL * RPL;
+  static constexpr int RSTEP = 2 * RPL;
   static constexpr int L0 = NKS * RSTEP;         // two left tiles (128 rows, h + m planes)
   static constexpr int LPL = 128 * 32;
-  static constexpr int LBUF = NPL * LPL;
+  static constexpr int LBUF = 2 * LPL;
   static constexpr int SH0 = L0 + 2 * LBUF;      // the compute waves' shear rings
   static constexpr int SHW = FUSE == 2 ? 0 : 3 * kSlot;
-  // volume-free pass (FUSE 2): the compute wave folds its first blocks and dumps the last FB
-  // blocks with its partial state (m, s, tt) for the memory wave of its SIMD to finish; one dump
-  // buffer per wave (two, alternating, when every step is a pass's first step)
-  static constexpr int NBUF = NKS == 1 ? 2 : 1;
-  static constexpr int DSTATE = 2048;            // m[64], s[64], tt[64]
-  static constexpr int FB = [] {
-    if (FUSE != 2 || !SMCV_SL_OFFLOAD) return 0;
-    if (NKS == 1 && NP == 1 && TMAX == 7) return 0;  // (its compute wave would spill)
-    int fb = TMAX - 1;
-    while (fb > 0 && L0 + 2 * LBUF + NBUF * kCW * (fb * kSlot + DSTATE) + 24 * 4 > 160 * 1024) --fb;
-    return fb;
-  }();
-  static constexpr int DW = FB > 0 ? FB * kSlot + DSTATE : 0;  // one wave's dump buffer
-  static constexpr int MAXW = SH0 + kCW * SHW + NBUF * kCW * DW;  // maxima: max|L| of 8
-  static constexpr size_t SHM = (size_t)MAXW + 24 * 4;  // segments, max|R| of the two 64-column
-                                                        // halves of 8 pieces
+  static constexpr int MAXW = SH0 + kCW * SHW;   // maxima: max|L| of 8 segments, max|R| of the
+  static constexpr size_t SHM = (size_t)MAXW + 24 * 4;  // two 64-column halves of 8 pieces
   static_assert(SHM <= 160 * 1024, "one workgroup per CU");
   static_assert(NKS == 1 || NKS % 2 == 0, "channel steps");
   static_assert(NP == 1 || NKS == 1, "two D passes keep one channel step's windows");
@@ -122,14 +105,10 @@ constexpr Task r_task(int q) {
 constexpr int pmod(int a, int m) { return ((a % m) + m) % m; }
 }  // namespace slide
 
-template <bool CW, bool MEAN, int TMAX, int NKS, int NP, int NSETS, int FUSE, typename TI>
+template <bool CW, bool MEAN, int TMAX, int NKS, int NP, int NSETS, int FUSE>
 __device__ __forceinline__ void sl_role(const Args& args, unsigned char* smem) {
   using namespace slide;
-  // TI: the feature type -- fp32 (the two-plane split, three products per block and step) or
-  // fp16 / bf16 (one plane as it is, one exact product; the volume-free fused pass only)
-  constexpr bool F32 = std::is_same<TI, float>::value;
-  static_assert(F32 || FUSE == 2, "16-bit features: the volume-free fused pass only");
-  using G = Geo<TMAX, NKS, NP, FUSE, F32 ? 2 : 1>;
+  using G = Geo<TMAX, NKS, NP, FUSE>;
   constexpr bool VOL = FUSE != 2;
   constexpr int T = TMAX;
   constexpr int DMAX = G::DMAX;
@@ -141,8 +120,8 @@ __device__ __forceinline__ void sl_role(const Args& args, unsigned char* smem) {
   constexpr bool CHECK_FIRST = NKS == 1;
   static_assert(T >= 5, "the 3-slot shear ring needs blocks T-1 .. 0 to reach chunk T-4 >= 1");
   constexpr bool isC = CW;
-  const TI* __restrict__ L = static_cast<const TI*>(args.L);
-  const TI* __restrict__ R = static_cast<const TI*>(args.R);
+  const float* __restrict__ L = static_cast<const float*>(args.L);
+  const float* __restrict__ R = static_cast<const float*>(args.R);
   const int H = args.H, W = args.W, D = args.D;
   const Strides4 ls = args.ls, rs = args.rs;
 
@@ -202,19 +181,18 @@ __device__ __forceinline__ void sl_role(const Args& args, unsigned char* smem) {
   const unsigned o_blk = (unsigned)swz(4 * (gq & 7), wp) + 8u * (unsigned)c4;
   const unsigned o_l = (unsigned)swz(4 * gq, wp) + 8u * (unsigned)c4;
 
-  using QT = typename Quad<TI>::type;  // 4 pixels of one channel row: 16 B fp32, 8 B 16-bit
-  QT sv[NSETS][4];
+  f32x4v sv[NSETS][4];
   bool okp[NSETS];
   auto load = [&](int set, const Work& k, int kc) __attribute__((always_inline)) {
     const int px = k.x0 + 4 * gq;
     okp[set] = px < W;
     const int pxc = min(px, W - 4);  // pad groups (x >= W): a valid group, staged as zeros
-    const TI* p = (isR ? R + (int64_t)k.n * rs.n + (int64_t)k.y * rs.h
+    const float* p = (isR ? R + (int64_t)k.n * rs.n + (int64_t)k.y * rs.h
                           : L + (int64_t)k.n * ls.n + (int64_t)k.y * ls.h) +
                      pxc + (int64_t)(kc * kKC + chl) * cs;
     int64_t csl = cs;
     asm volatile("" : "+v"(csl));
-    if constexpr ((SMCV_SL_ABLATE & 4) && F32) {
+    if constexpr (SMCV_SL_ABLATE & 4) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         sv[set][j] = f32x4v{1.f, -1.f, 0.5f, 2.f};
@@ -228,7 +206,7 @@ __device__ __forceinline__ void sl_role(const Args& args, unsigned char* smem) {
       if constexpr (SMCV_SL_NTLOAD) {
         typedef __attribute__((address_space(1))) const void gcvoid;
         sv[set][j] = __builtin_nontemporal_load(
-            reinterpret_cast<__attribute__((address_space(1))) const QT*>((gcvoid*)p));
+            reinterpret_cast<__attribute__((address_space(1))) const f32x4v*>((gcvoid*)p));
       } else {
         gload<false>(sv[set][j], p);
       }
@@ -241,27 +219,6 @@ __device__ __forceinline__ void sl_role(const Args& args, unsigned char* smem) {
   // at + poff); keep = false: compute nothing but the loads' consumption (a half-piece's other
   // half, which must not be written)
   auto stage = [&](int set, unsigned dst, unsigned poff, bool keep) __attribute__((always_inline)) {
-    if constexpr (!F32) {
-      // 16-bit features as they are (no scale, maxima stay 0): pixel p's 4 channels -> 8 B of
-      // the one plane (pad groups zeroed: they reach only cells x < d or columns x >= W)
-      (void)poff;
-      u32x2 qv[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) qv[j] = okp[set] ? sv[set][j] : u32x2{0u, 0u};
-      unsigned o0 = dst;
-      asm volatile("" : "+v"(o0));
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        // channels 2i (low half), 2i + 1 (high half) of pixel p
-        const unsigned lo0 = p < 2 ? qv[0].x : qv[0].y, hi0 = p < 2 ? qv[1].x : qv[1].y;
-        const unsigned lo1 = p < 2 ? qv[2].x : qv[2].y, hi1 = p < 2 ? qv[3].x : qv[3].y;
-        const unsigned sel = (p & 1) ? 0x07060302u : 0x05040100u;
-        const u32x2 w = {__builtin_amdgcn_perm(hi0, lo0, sel), __builtin_amdgcn_perm(hi1, lo1, sel)};
-        if (keep && !(SMCV_SL_ABLATE & 16))
-          *reinterpret_cast<__attribute__((address_space(3))) u32x2*>(o0 ^ (32u * p)) = w;
-      }
-      return;
-    } else {
     f32x4v(&x)[4] = sv[set];
     float m0 = 0.f, m1 = 0.f;
 #pragma unroll
@@ -286,7 +243,6 @@ __device__ __forceinline__ void sl_role(const Args& args, unsigned char* smem) {
         *reinterpret_cast<__attribute__((address_space(3))) u32x2*>(a1) = u32x2{wh.z, wh.w};
         *reinterpret_cast<__attribute__((address_space(3))) u32x2*>(a1 + poff) = u32x2{wm.z, wm.w};
       }
-    }
     }
   };
   // LDS destination of a right-column task: piece sigma (blocks 4 sigma .. 4 sigma + 3), channel
@@ -443,80 +399,17 @@ __device__ __forceinline__ void sl_role(const Args& args, unsigned char* smem) {
   // FUSE: the previous pass's soft-argmin straight from the accumulators (band_common.h), before
   // the next pass's first MFMAs overwrite them; nothing for an invalid segment.  Two D passes
   // without the volume: pass 0's state waits in registers for pass 1.
-  // The previous pass's soft-argmin straight from the accumulators (band_common.h), before the
-  // next pass's first MFMAs overwrite them; nothing for an invalid segment.  Two D passes: pass
-  // 0's state waits in registers for pass 1.  With the fold offload (G::FB > 0) the compute wave
-  // folds blocks [0, T - FB) and dumps the rest with its partial state; mem_fold finishes.
-  // 16-bit features under autocast (args.round): each cell rounded to the feature dtype first,
-  // as the reference's volume holds it.
-  using RT = typename std::conditional<F32, float, TI>::type;
-  constexpr int FB = G::FB;
-  [[maybe_unused]] int dpar = 0;  // the dump buffer the next dump goes to (NBUF = 2)
-  // SCALE / XLT as compile-time forms of one uniform choice
-  auto with_forms = [&](int kk, int js, auto&& f) __attribute__((always_inline)) {
-    const bool sc = kk != 0, xl = js < 0;
-    if (!sc && !xl)
-      f(std::false_type{}, std::false_type{});
-    else if (sc && !xl)
-      f(std::true_type{}, std::false_type{});
-    else if (!sc)
-      f(std::false_type{}, std::true_type{});
-    else
-      f(std::true_type{}, std::true_type{});
-  };
-  // the pass state the memory wave folds next (copied at the dump; workgroup-uniform)
-  [[maybe_unused]] Work fq = pw;
-  [[maybe_unused]] int fq_kk = 0, fq_valid = 0;
-  auto dump_base = [&](int b, int w) -> unsigned {
-    return sbase + (unsigned)(G::SH0 + (b * kCW + w) * G::DW);
-  };
   auto fuse_regs = [&]() __attribute__((always_inline)) {
     if constexpr (FUSE != 0) {
-      if constexpr (FB > 0) {  // (FUSE 2) partial fold + dump
-        const int b = G::NBUF == 2 ? dpar : 0;
-        if (p_bytes != 0) {
-          with_forms(p_kk, pw.js, [&](auto scale, auto xlt) __attribute__((always_inline)) {
-            constexpr bool SC = decltype(scale)::value, XL = decltype(xlt)::value;
-            // the dumped blocks first (their registers are free during the fold)
-            const unsigned db = dump_base(b, rw);
-#pragma unroll
-            for (int f = 0; f < FB; ++f)
-#pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                const f32x4v v = {acc[T - FB + f][4 * q], acc[T - FB + f][4 * q + 1],
-                                  acc[T - FB + f][4 * q + 2], acc[T - FB + f][4 * q + 3]};
-                *reinterpret_cast<__attribute__((address_space(3))) f32x4v*>(
-                    db + (unsigned)(f * kSlot + q * 1024 + 16 * lane)) = v;
-              }
-            float m = -INFINITY;
-            double s = 0.0, t = 0.0;
-            if (!F32 && args.round)
-              fold_blocks<T, MEAN, SC, XL, RT, 0, T - FB>(acc, args, pw, -p_kk, 0, rw, lr, hh, m, s, t);
-            else
-              fold_blocks<T, MEAN, SC, XL, float, 0, T - FB>(acc, args, pw, -p_kk, 0, rw, lr, hh, m, s, t);
-            const unsigned sb = db + (unsigned)(FB * kSlot);
-            *reinterpret_cast<__attribute__((address_space(3))) float*>(sb + 4 * lane) = m;
-            *reinterpret_cast<__attribute__((address_space(3))) double*>(sb + 256 + 8 * lane) = s;
-            *reinterpret_cast<__attribute__((address_space(3))) double*>(sb + 768 + 8 * lane) = t;
-          });
-        }
-        return;
-      }
       if (p_bytes == 0) return;
-      with_forms(p_kk, pw.js, [&](auto scale, auto xlt) __attribute__((always_inline)) {
+      auto go = [&](auto scale, auto xlt) __attribute__((always_inline)) {
         constexpr bool SC = decltype(scale)::value, XL = decltype(xlt)::value;
         if constexpr (NP == 1) {
-          if (!F32 && args.round)
-            fused_softargmin<T, MEAN, SC, XL, false, RT>(acc, args, pw, -p_kk, 0, rw, lr, hh);
-          else
-            fused_softargmin<T, MEAN, SC, XL, false>(acc, args, pw, -p_kk, 0, rw, lr, hh);
+          fused_softargmin<T, MEAN, SC, XL, false>(acc, args, pw, -p_kk, 0, rw, lr, hh);
         } else {
           float m;
           double s, t;
-          if (!F32 && args.round)
-            fused_softargmin_state<T, MEAN, SC, XL, RT>(acc, args, pw, -p_kk, 0, rw, lr, hh, m, s, t);
-          else
-            fused_softargmin_state<T, MEAN, SC, XL>(acc, args, pw, -p_kk, 0, rw, lr, hh, m, s, t);
+          fused_softargmin_state<T, MEAN, SC, XL>(acc, args, pw, -p_kk, 0, rw, lr, hh, m, s, t);
           if (pw.pass == 0) {
             f_m = m;
             f_s = s;
@@ -525,76 +418,17 @@ __device__ __forceinline__ void sl_role(const Args& args, unsigned char* smem) {
             fused_two_pass_store(args, pw, rw, lr, hh, f_m, f_s, f_t, m, s, t);
           }
         }
-      });
+      };
+      const bool sc = p_kk != 0, xl = pw.js < 0;
+      if (!sc && !xl)
+        go(std::false_type{}, std::false_type{});
+      else if (sc && !xl)
+        go(std::true_type{}, std::false_type{});
+      else if (!sc)
+        go(std::false_type{}, std::true_type{});
+      else
+        go(std::true_type{}, std::true_type{});
     }
-  };
-  // the memory wave's share of the offloaded fold: blocks [T - FB + F0, T - FB + F1) of the
-  // dump in buffer b from its partner compute wave (mw); LAST: merge the pair, store (or keep
-  // pass 0's state for pass 1)
-  [[maybe_unused]] float q_m = 0.f;
-  [[maybe_unused]] double q_s = 0.0, q_t = 0.0;
-  auto mem_fold = [&]<int F0, int F1, bool LAST>(int b) __attribute__((always_inline)) {
-    if constexpr (FB > 0 && !isC) {
-      if (fq_valid == 0) return;
-      const unsigned db = dump_base(b, mw);
-      if constexpr (F0 == 0) {
-        const unsigned sb = db + (unsigned)(FB * kSlot);
-        q_m = *reinterpret_cast<__attribute__((address_space(3))) float*>(sb + 4 * lane);
-        q_s = *reinterpret_cast<__attribute__((address_space(3))) double*>(sb + 256 + 8 * lane);
-        q_t = *reinterpret_cast<__attribute__((address_space(3))) double*>(sb + 768 + 8 * lane);
-      }
-      f32x16 blk[F1 - F0 > 0 ? F1 - F0 : 1];
-#pragma unroll
-      for (int f = 0; f < F1 - F0; ++f)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const f32x4v v = *reinterpret_cast<__attribute__((address_space(3))) f32x4v*>(
-              db + (unsigned)((F0 + f) * kSlot + q * 1024 + 16 * lane));
-          blk[f][4 * q] = v.x;
-          blk[f][4 * q + 1] = v.y;
-          blk[f][4 * q + 2] = v.z;
-          blk[f][4 * q + 3] = v.w;
-        }
-      with_forms(fq_kk, fq.js, [&](auto scale, auto xlt) __attribute__((always_inline)) {
-        constexpr bool SC = decltype(scale)::value, XL = decltype(xlt)::value;
-        if (!F32 && args.round)
-          fold_blocks<T, MEAN, SC, XL, RT, T - FB + F0, T - FB + F1>(blk, args, fq, -fq_kk, 0, mw, lr, hh,
-                                                                     q_m, q_s, q_t);
-        else
-          fold_blocks<T, MEAN, SC, XL, float, T - FB + F0, T - FB + F1>(blk, args, fq, -fq_kk, 0, mw, lr,
-                                                                        hh, q_m, q_s, q_t);
-      });
-      if constexpr (LAST) {
-        float M;
-        fold_pair_merge(q_m, q_s, q_t, M);
-        if constexpr (NP == 1) {
-          const int x = fq.x0 + 32 * mw + lr;
-          if (hh == 0 && x < args.W)
-            store_one<float>(args.disp + ((size_t)fq.n * args.H + fq.y) * args.W + x, (float)(q_t / q_s));
-        } else {
-          const double tg = q_t + (double)fq.dp * q_s;
-          if (fq.pass == 0) {
-            f_m = M;
-            f_s = q_s;
-            f_t = tg;
-          } else {
-            fused_two_pass_store(args, fq, mw, lr, hh, f_m, f_s, f_t, M, q_s, tg);
-          }
-        }
-      }
-    }
-  };
-  // the whole dump in chunks of two blocks (fewer registers live at once)
-  auto mem_fold_all = [&](int b) __attribute__((always_inline)) {
-    [&]<int... C_>(std::integer_sequence<int, C_...>) __attribute__((always_inline)) {
-      (mem_fold.template operator()<2 * C_, (2 * C_ + 2 < FB ? 2 * C_ + 2 : FB), (2 * C_ + 2 >= FB)>(b), ...);
-    }(std::make_integer_sequence<int, (FB + 1) / 2>{});
-  };
-  // both roles: what the next dump holds (recorded when the compute wave dumps it)
-  auto note_dump = [&]() __attribute__((always_inline)) {
-    fq = pw;
-    fq_kk = p_kk;
-    fq_valid = p_bytes != 0;
   };
 
   auto barrier = []() __attribute__((always_inline)) {
@@ -634,11 +468,9 @@ __device__ __forceinline__ void sl_role(const Args& args, unsigned char* smem) {
   // (SPEC: a workgroup-uniform branch around each block's ring writes only; a whole second copy
   // of the step, MFMAs included, made the register allocator spill at the join)
   auto matrix = [&]<int KS, bool SHEAR>(unsigned lb) __attribute__((always_inline)) {
-    using FV = typename std::conditional<std::is_same<TI, __bf16>::value, bf16x8, f16x8>::type;
     const unsigned char* bb = smem + lb + 32 * rw * 32 + swz(lr, hh);
-    const FV bh = *reinterpret_cast<const FV*>(bb);
-    [[maybe_unused]] f16x8 bmv;
-    if constexpr (F32) bmv = *reinterpret_cast<const f16x8*>(bb + G::LPL);
+    const f16x8 bh = *reinterpret_cast<const f16x8*>(bb);
+    const f16x8 bmv = *reinterpret_cast<const f16x8*>(bb + G::LPL);
     const unsigned char* rk = smem + KS * G::RSTEP + swz(lr, hh);
     [[maybe_unused]] f32x4v cv[4];
     [&]<int... K_>(std::integer_sequence<int, K_...>) __attribute__((always_inline)) {
@@ -651,9 +483,8 @@ __device__ __forceinline__ void sl_role(const Args& args, unsigned char* smem) {
             unsigned ao = rslot(t);
             asm volatile("" : "+v"(ao));
             const unsigned char* ab = rk + ao;
-            const FV ah = *reinterpret_cast<const FV*>(ab);
-            [[maybe_unused]] f16x8 am;
-            if constexpr (F32) am = *reinterpret_cast<const f16x8*>(ab + G::RPL);
+            const f16x8 ah = *reinterpret_cast<const f16x8*>(ab);
+            const f16x8 am = *reinterpret_cast<const f16x8*>(ab + G::RPL);
             if constexpr (SHEAR && VOL) {
               if constexpr (cr >= 0) drain_read.template operator()<cr>(cv);
               if (__builtin_expect(p_special, 0))
@@ -661,13 +492,7 @@ __device__ __forceinline__ void sl_role(const Args& args, unsigned char* smem) {
               else
                 write_block.template operator()<t, false>();
             }
-            if constexpr (!F32) {  // 16-bit features: one exact product
-              const f32x16 c0v = KS == 0 ? f32x16{} : acc[t];
-              if constexpr (std::is_same<TI, __bf16>::value)
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, c0v, 0, 0, 0);
-              else
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, c0v, 0, 0, 0);
-            } else if constexpr (SMCV_SL_ABLATE & 8) {
+            if constexpr (SMCV_SL_ABLATE & 8) {
               asm volatile("" : : "v"(ah), "v"(am), "v"(bh), "v"(bmv));
             } else {
               f32x16 c;
@@ -729,18 +554,6 @@ __device__ __forceinline__ void sl_role(const Args& args, unsigned char* smem) {
       } else {
         if constexpr (tlL.has) load(GL % NSETS, wq[segl + tlL.del], tlL.kc);
       }
-      // (volume-free pass) the memory wave's share of the previous pass's fold: the dump of the
-      // step before (one channel step), or spread over steps 1 .. NKS-1 of the pass
-      if constexpr (FB > 0) {
-        if constexpr (NKS == 1) {
-          mem_fold_all(dpar ^ 1);
-        } else if constexpr (KS >= 1) {
-          constexpr int c = (FB + NKS - 2) / (NKS - 1);
-          constexpr int F0 = (KS - 1) * c < FB ? (KS - 1) * c : FB;
-          constexpr int F1 = KS * c < FB ? KS * c : FB;
-          if constexpr (F0 < F1) mem_fold.template operator()<F0, F1, F1 == FB>(0);
-        }
-      }
       // this step's tasks
       constexpr Task sL = l_task<NKS, NP>(q), sR = r_task<NKS, NP>(q);
       if (isR) {
@@ -758,17 +571,12 @@ __device__ __forceinline__ void sl_role(const Args& args, unsigned char* smem) {
         }
       }
     }
-    if constexpr (FB > 0 && KS == 0) {  // both roles: what this step's dump holds
-      note_dump();
-      if constexpr (G::NBUF == 2) dpar ^= 1;
-    }
     if constexpr (!(SMCV_SL_ABLATE & 32)) barrier();
     if constexpr (NP == 1) lpar ^= 1;
   };
 
   // exact fp32 FMA path for a segment holding a non-finite value or out of the scale range
   auto slow_segment = [&](const Work& k0) __attribute__((always_inline)) {
-    if constexpr (!F32) return;  // 16-bit features: no scale, the maxima stay 0 (never taken)
     if constexpr (FUSE != 0) {  // every disparity of the segment (both passes at once)
       Work kd = k0;
       kd.dp = 0;
@@ -780,8 +588,8 @@ __device__ __forceinline__ void sl_role(const Args& args, unsigned char* smem) {
       if constexpr (VOL) {
         const float mul = MEAN ? args.mul : 1.0f;
         float* out = static_cast<float*>(args.out);
-        const float* lrow = reinterpret_cast<const float*>(L) + (int64_t)k.n * ls.n + (int64_t)k.y * ls.h;
-        const float* rrow = reinterpret_cast<const float*>(R) + (int64_t)k.n * rs.n + (int64_t)k.y * rs.h;
+        const float* lrow = L + (int64_t)k.n * ls.n + (int64_t)k.y * ls.h;
+        const float* rrow = R + (int64_t)k.n * rs.n + (int64_t)k.y * rs.h;
         for (int idx = tid; idx < k.Dp * kXT; idx += kThreads) {
           const int dl = idx / kXT, x = k.x0 + idx % kXT, d = k.dp + dl;
           if (x >= W) continue;
@@ -958,15 +766,8 @@ __device__ __forceinline__ void sl_role(const Args& args, unsigned char* smem) {
       if (done) return;
     }
   }();
-  // the last pass: into the ring, then out (volume-free with the fold offload: the pending dump,
-  // then the last pass's dump, folded by the memory waves after one more barrier)
-  if constexpr (FB > 0) {
-    if constexpr (isC) fuse_regs();
-    if constexpr (G::NBUF == 2) mem_fold_all(dpar ^ 1);
-    note_dump();
-    barrier();
-    mem_fold_all(dpar);
-  } else if constexpr (isC) {
+  // the last pass: into the ring, then out
+  if constexpr (isC) {
     fuse_regs();
     if constexpr (VOL) {
       auto shear_out = [&]<bool SPEC>() __attribute__((always_inline)) {
@@ -995,30 +796,30 @@ __device__ __forceinline__ void sl_role(const Args& args, unsigned char* smem) {
 }
 
 // FUSE 0: the volume; 1: the volume and its soft-argmin; 2: the soft-argmin only
-template <bool MEAN, int TMAX, int NKS, int NP, int NSETS, int FUSE, typename TI = float>
+template <bool MEAN, int TMAX, int NKS, int NP, int NSETS, int FUSE>
 __global__ __launch_bounds__(slide::kThreads, 1) void band_sl(Args args) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) < slide::kCW) {
 #if SMCV_SL_DIAG_ROLE != 2  // (register-usage diagnostics only: 1 compute role alone, 2 memory)
-    sl_role<true, MEAN, TMAX, NKS, NP, NSETS, FUSE, TI>(args, smem);
+    sl_role<true, MEAN, TMAX, NKS, NP, NSETS, FUSE>(args, smem);
 #endif
   } else {
 #if SMCV_SL_DIAG_ROLE != 1
-    sl_role<false, MEAN, TMAX, NKS, NP, NSETS, FUSE, TI>(args, smem);
+    sl_role<false, MEAN, TMAX, NKS, NP, NSETS, FUSE>(args, smem);
 #endif
   }
 }
 
-template <bool MEAN, int TMAX, int NKS, int NP, int NSETS, int FUSE, typename TI = float>
+template <bool MEAN, int TMAX, int NKS, int NP, int NSETS, int FUSE>
 int launch_sl(Args a, int64_t N, hipStream_t st) {
-  using G = slide::Geo<TMAX, NKS, NP, FUSE, std::is_same<TI, float>::value ? 2 : 1>;
+  using G = slide::Geo<TMAX, NKS, NP, FUSE>;
   a.tiles = (int)ceil_div(a.W, kXT);
   const int64_t rows = (int64_t)a.H * N;
   if (rows * a.tiles > INT32_MAX / 64) return fail(SM_EINVAL, "band kernel: too much work for one launch");
   a.nwork = (int)rows;
   a.fd_tiles = make_fastdiv((unsigned)a.tiles);
   a.fd_h = make_fastdiv((unsigned)a.H);
-  auto kern = band_sl<MEAN, TMAX, NKS, NP, NSETS, FUSE, TI>;
+  auto kern = band_sl<MEAN, TMAX, NKS, NP, NSETS, FUSE>;
   static std::atomic<unsigned long long> lds_done{0};
   const int dev = stream_device(st);
   if (int rc = ensure_lds_limit(reinterpret_cast<const void*>(kern), (int)G::SHM, dev, lds_done))
@@ -1082,51 +883,6 @@ int band_sl_run(const Args& a0, int64_t N, bool mean, bool aligned4, hipStream_t
   if (np == 2) return go(T5{}, I1{}, I2{});
   if (a.pw <= 128) return nks == 1 ? go(T5{}, I1{}, I1{}) : go(T5{}, I4{}, I1{});
   return nks == 1 ? go(T7{}, I1{}, I1{}) : go(T7{}, I4{}, I1{});
-}
-
-// The volume-free fused pass (FUSE 2) of fp16 / bf16 features with fp32 disparities on the
-// sliding-window kernel (SM_FUSED_DISP_F32; args.round: the cells rounded to the feature dtype
-// before the fold); *handled = false when the shape is not one it takes: 4-element aligned rows
-// of W >= 4, C = 16 NKS with NKS in {1, 2, 4}; one D pass of 65..192, or (C = 16) two passes of
-// pw = 32 m <= 128 (D <= 256).
-int band_sl_half_run(const Args& a0, int64_t N, bool mean, int dtype, hipStream_t st,
-                     bool* handled) {
-  *handled = false;
-  Args a = a0;
-  const int nks = a.cpg / 16;
-  if ((dtype != SM_F16 && dtype != SM_BF16) || a.G != 1 || a.W < 4 || a.cpg % 16 != 0 ||
-      (nks != 1 && nks != 2 && nks != 4))
-    return SM_OK;
-  int np = 1;
-  if (a.npass == 1) {
-    if (a.pw <= 64 || a.pw > 192) return SM_OK;
-  } else {
-    const int pw2 = (int)((ceil_div(a.D, 2) + 31) / 32 * 32);
-    if (nks != 1 || a.D > 256 || a.D <= 192 || pw2 > 128) return SM_OK;
-    a.npass = 2;
-    a.pw = pw2;
-    np = 2;
-  }
-  *handled = true;
-  auto go = [&](auto tm, auto nk, auto npc, auto ti) {
-    constexpr int TM = decltype(tm)::value, NK = decltype(nk)::value, NPC = decltype(npc)::value;
-    using TI = typename decltype(ti)::type;
-    constexpr int NS = NK == 1 ? 2 : 4;
-    return mean ? launch_sl<true, TM, NK, NPC, NS, 2, TI>(a, N, st)
-                : launch_sl<false, TM, NK, NPC, NS, 2, TI>(a, N, st);
-  };
-  auto by_t = [&](auto ti) {
-    using I1 = std::integral_constant<int, 1>;
-    using I2 = std::integral_constant<int, 2>;
-    using I4 = std::integral_constant<int, 4>;
-    using T5 = std::integral_constant<int, 5>;
-    using T7 = std::integral_constant<int, 7>;
-    if (np == 2) return go(T5{}, I1{}, I2{}, ti);
-    if (a.pw <= 128)
-      return nks == 1 ? go(T5{}, I1{}, I1{}, ti) : nks == 2 ? go(T5{}, I2{}, I1{}, ti) : go(T5{}, I4{}, I1{}, ti);
-    return nks == 1 ? go(T7{}, I1{}, I1{}, ti) : nks == 2 ? go(T7{}, I2{}, I1{}, ti) : go(T7{}, I4{}, I1{}, ti);
-  };
-  return dtype == SM_F16 ? by_t(std::type_identity<__half>{}) : by_t(std::type_identity<__bf16>{});
 }
 
 }  // namespace h2band

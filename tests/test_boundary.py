@@ -56,7 +56,7 @@ def test_error_path_without_gpu_work():
     assert b"W stride" in lib.sm_last_error()
     rc = lib.sm_cv_groupwise(1, 1, 1, _lib.SM_F32, 1, 16, 2, 8, 4, 3, None, None, None)
     assert rc == _lib.SM_EINVAL and b"C % G" in lib.sm_last_error()
-    rc = lib.sm_cv_inner_product_softargmin(1, 1, 1, 1, _lib.SM_F32, 1, 2, 3, 4, 5, None, None, 7,
+    rc = lib.sm_cv_inner_product_softargmin(1, 1, 1, 1, _lib.SM_F32, 1, 2, 3, 4, 5, None, None, 8,
                                             None)
     assert rc == _lib.SM_EINVAL and b"mode" in lib.sm_last_error()
     rc = lib.sm_cv_concat(1, 1, 1, 7, 1, 2, 3, 4, 5, None, None, None)
