@@ -433,7 +433,7 @@ def cpu_baseline(cfg, a, seconds):
 
 
 # ----------------------------------------------------------------------------- PMC traffic
-EVIDENCE_ROUND = "r04"
+EVIDENCE_ROUND = "r05"
 
 
 def evidence_name(a):

@@ -20,7 +20,7 @@ import os
 import re
 import sys
 
-KEEP = ("band_h2", "band_sp", "band_rs", "softargmin", "argext", "concat_kernel", "shifted_rows_kernel", "interweave_kernel",
+KEEP = ("band_h2", "band_sl", "band_rs", "softargmin", "argext", "concat_kernel", "shifted_rows_kernel", "interweave_kernel",
         "dot_volume", "ip_", "warp")
 
 
