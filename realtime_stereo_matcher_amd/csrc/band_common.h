@@ -287,6 +287,9 @@ __device__ __forceinline__ int exp_of(float x) { return __builtin_amdgcn_frexp_e
 #ifndef SMCV_SCHED_PHASE
 #define SMCV_SCHED_PHASE 0
 #endif
+#ifndef SMCV_SCHED_IL
+#define SMCV_SCHED_IL 0  // diagnostic: chunks of IL segments dealt round-robin to the XCD groups
+#endif                   // instead of one contiguous range each (IL a multiple of 8)
 struct Sched {
   int gi, gsz, sbeg, scnt, nitems, npass, phase;
   bool rot, none;
@@ -299,12 +302,24 @@ struct Sched {
     const int q = nseg >> 3, rr = nseg & 7;
     sbeg = grp < rr ? grp * (q + 1) : rr * (q + 1) + (grp - rr) * q;
     scnt = q + (grp < rr ? 1 : 0);
+    if constexpr (SMCV_SCHED_IL > 0) {
+      const int nch = (nseg + SMCV_SCHED_IL - 1) / SMCV_SCHED_IL;
+      const int mine = nch > grp ? (nch - grp + 7) / 8 : 0;
+      const int last = nseg - (nch - 1) * SMCV_SCHED_IL;  // the last chunk's segments
+      sbeg = grp;
+      scnt = mine * SMCV_SCHED_IL - (((nch - 1) & 7) == grp ? SMCV_SCHED_IL - last : 0);
+    }
     none = gi >= scnt;  // the whole workgroup leaves together
     nitems = none ? 0 : ((scnt - gi + gsz - 1) / gsz) * np;
     rot = (gsz & 7) == 0;
     // diagnostic: start each XCD's walk at a different point of its range (a rotation, so every
     // segment is still taken once), so the eight XCDs' streams are not a fixed stride apart
     phase = SMCV_SCHED_PHASE == 0 ? 0 : (int)(((long long)scnt * grp / (8 * SMCV_SCHED_PHASE)) & ~7);
+  }
+  __device__ __forceinline__ int seg_of(int local) const {
+    if constexpr (SMCV_SCHED_IL > 0)  // sbeg = the group: chunk local / IL is global chunk grp + 8 (local / IL)
+      return (sbeg + 8 * (local / SMCV_SCHED_IL)) * SMCV_SCHED_IL + local % SMCV_SCHED_IL;
+    return sbeg + local;
   }
   __device__ __forceinline__ int rotate(int local) const {
     if (SMCV_SCHED_PHASE == 0) return local;
@@ -316,7 +331,7 @@ struct Sched {
     const int p = i - si * npass;
     const int j = gi + si * gsz;
     const int b = j & ~7;
-    const int seg = sbeg + rotate((rot && b + 8 <= scnt) ? (b | ((j + si) & 7)) : j);
+    const int seg = seg_of(rotate((rot && b + 8 <= scnt) ? (b | ((j + si) & 7)) : j));
     return seg * npass + p;
   }
   __device__ __forceinline__ int item(int i) const {
@@ -324,7 +339,7 @@ struct Sched {
     const int p = i - si * npass;
     const int j = gi + si * gsz;
     const int b = j & ~7;
-    const int seg = sbeg + rotate((rot && b + 8 <= scnt) ? (b | ((j + si) & 7)) : j);
+    const int seg = seg_of(rotate((rot && b + 8 <= scnt) ? (b | ((j + si) & 7)) : j));
     return seg * npass + p;
   }
 };

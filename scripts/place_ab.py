@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--pairs", type=int, default=32)
     ap.add_argument("--reps", type=int, default=6)
     ap.add_argument("--seq", type=int, default=0, help="instead: time K buffers allocated in a row")
+    ap.add_argument("--patterns", action="store_true", help="--order: also zero_ and soft_argmin")
     ap.add_argument("--order", default="", help="instead: allocation order, e.g. F,S1024,V,V (F: the "
                     "features, V: a volume buffer, S<MiB>: a spacer); every V timed")
     a = ap.parse_args()
@@ -81,6 +82,8 @@ def main():
         for r in range(2):
             for i, b in enumerate(vols):
                 rep(f"{a.order}: V{i} round {r}", [timed(b.data_ptr()) for _ in range(a.reps)], b.data_ptr())
+                if not a.patterns:
+                    continue
                 # the same buffer under a sequential fill and under the regression's plane walk
                 rep(f"{a.order}: V{i} zero_", [op_time(b.zero_) for _ in range(a.reps)], b.data_ptr())
                 rep(f"{a.order}: V{i} soft_argmin", [op_time(lambda: F.soft_argmin(b)) for _ in range(a.reps)],
