@@ -27,19 +27,43 @@ def main():
     ap.add_argument("--seq", type=int, default=0, help="instead: time K buffers allocated in a row")
     ap.add_argument("--patterns", action="store_true", help="--order: also zero_ and soft_argmin")
     ap.add_argument("--order", default="", help="instead: allocation order, e.g. F,S1024,V,V (F: the "
-                    "features, V: a volume buffer, S<MiB>: a spacer); every V timed")
+                    "features, V: a volume buffer (torch), H: one from hipMalloc, C: one from "
+                    "hipExtMallocWithFlags(contiguous), S<MiB>: a spacer); every V / H / C timed")
     a = ap.parse_args()
     n, c, h, w, D = a.pairs, 64, 540, 960, 192
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     held, vols = [], []
     L = R = None
+    raw = []  # (ptr) from hipMalloc / hipExtMallocWithFlags, freed at the end
+    vb0 = n * D * h * w * 4
+
+    class _Raw:  # a volume-sized buffer outside torch's allocator
+        def __init__(self, flags):
+            import ctypes
+            self.hip = ctypes.CDLL("libamdhip64.so")
+            self.p = ctypes.c_void_p()
+            if flags < 0:
+                rc = self.hip.hipMalloc(ctypes.byref(self.p), ctypes.c_size_t(vb0))
+            else:
+                rc = self.hip.hipExtMallocWithFlags(ctypes.byref(self.p), ctypes.c_size_t(vb0), ctypes.c_uint(flags))
+            if rc != 0:
+                raise RuntimeError(f"hip allocation failed ({rc})")
+            raw.append(self)
+
+        def data_ptr(self):
+            return self.p.value
+
     for tok in (a.order.split(",") if a.order else ["F"]):
         if tok == "F":
             L = torch.randn(n, c, h, w, device=dev, generator=g)
             R = torch.randn(n, c, h, w, device=dev, generator=g)
         elif tok == "V":
             vols.append(torch.empty(n, D, h, w, device=dev))
+        elif tok == "H":  # plain hipMalloc
+            vols.append(_Raw(-1))
+        elif tok == "C":  # hipExtMallocWithFlags(hipDeviceMallocContiguous)
+            vols.append(_Raw(4))
         else:
             held.append(torch.empty(int(tok[1:]) << 20, dtype=torch.uint8, device=dev))
     lib = _lib.load()
@@ -82,7 +106,7 @@ def main():
         for r in range(2):
             for i, b in enumerate(vols):
                 rep(f"{a.order}: V{i} round {r}", [timed(b.data_ptr()) for _ in range(a.reps)], b.data_ptr())
-                if not a.patterns:
+                if not a.patterns or isinstance(b, _Raw):
                     continue
                 # the same buffer under a sequential fill and under the regression's plane walk
                 rep(f"{a.order}: V{i} zero_", [op_time(b.zero_) for _ in range(a.reps)], b.data_ptr())
