@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--pairs", type=int, default=32)
     ap.add_argument("--reps", type=int, default=6)
     ap.add_argument("--seq", type=int, default=0, help="instead: time K buffers allocated in a row")
+    ap.add_argument("--algo", type=int, default=0, help="sm_ip_algo for sm_cv_inner_product_ex (0 auto)")
     ap.add_argument("--patterns", action="store_true", help="--order: also zero_ and soft_argmin")
     ap.add_argument("--order", default="", help="instead: allocation order, e.g. F,S1024,V,V (F: the "
                     "features, V: a volume buffer (torch), H: one from hipMalloc, C: one from "
@@ -71,9 +72,10 @@ def main():
     vb = n * D * h * w * 4
 
     def launch(ptr):
-        _lib.check(lib.sm_cv_inner_product(L.data_ptr(), R.data_ptr(), ptr, _lib.SM_F32, n, c, h, w, D,
-                                           _lib.strides_arg(L), _lib.strides_arg(R), st.cuda_stream),
-                   "sm_cv_inner_product")
+        _lib.check(lib.sm_cv_inner_product_ex(L.data_ptr(), R.data_ptr(), ptr, _lib.SM_F32, n, c, h, w, D,
+                                              _lib.strides_arg(L), _lib.strides_arg(R), a.algo,
+                                              st.cuda_stream),
+                   "sm_cv_inner_product_ex")
 
     def timed(ptr, after=None):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
