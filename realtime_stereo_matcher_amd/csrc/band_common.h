@@ -287,6 +287,10 @@ __device__ __forceinline__ int exp_of(float x) { return __builtin_amdgcn_frexp_e
 #ifndef SMCV_SCHED_PHASE
 #define SMCV_SCHED_PHASE 0
 #endif
+#ifndef SMCV_FOLD_FMA
+#define SMCV_FOLD_FMA 1  // fused fold of band_sl (and band_rs at C = 16): 1/C and 2^kk folded into
+#endif                   // the exponent's FMA (0: the cells scaled one by one; cfg4 volume-free 5 %
+                         // slower, r05)
 #ifndef SMCV_SCHED_IL
 #define SMCV_SCHED_IL 0  // diagnostic: chunks of IL segments dealt round-robin to the XCD groups
 #endif                   // instead of one contiguous range each (IL a multiple of 8)
@@ -410,6 +414,12 @@ __device__ __forceinline__ void slow_softargmin_f32(const Args& args, const Work
 // max(m, -FLT_MAX) keeps exp2 finite-argument when no cell is finite yet.  SCALE multiplies back
 // by 2^-(kL+kR); XLT forces the cells x < d (R pad rows) to 0, as the volume has them; RT (not
 // float): the cell rounded to RT first.
+// RT = FoldFma: the fp32 cells with 1/C and 2^kk folded into the exponent's FMA (the cells stay
+// raw; their block maximum is scaled once, K > 0 keeps it the maximum).  A kernel pair whose
+// volume-kept and volume-free calls must agree bit for bit uses the same RT.
+struct FoldFma {};
+using FoldF32 = std::conditional<SMCV_FOLD_FMA != 0, FoldFma, float>::type;
+
 template <int TMAX, bool MEAN, bool SCALE, bool XLT, typename RT, int t>
 __device__ __forceinline__ void fold_block(const f32x16& blk, const Args& args, const Work& k,
                                            int kL, int kR, int wave, int lr, int hh, float& m,
@@ -424,6 +434,37 @@ __device__ __forceinline__ void fold_block(const f32x16& blk, const Args& args, 
     asm volatile("" : "+v"(ub));
     float v[16];
     float bm = -INFINITY;
+    if constexpr (std::is_same<RT, FoldFma>::value) {
+      // the mean's 1/C and the scale 2^kk folded into the exponent's FMA: the cells stay raw,
+      // their maximum is scaled once (K > 0: monotonic), e = 2^(x K log2 e - max log2 e)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int ci = (i & 3) + 8 * (i >> 2);
+        float x = blk[i];
+        if constexpr (XLT) x = jlane + 32 * t + ci >= 0 ? x : 0.f;
+        if constexpr (decltype(maskc)::value) x = (unsigned)(ub - ci) < (unsigned)k.Dp ? x : -INFINITY;
+        v[i] = x;
+        bm = fmaxf(bm, x);
+      }
+      float K = MEAN ? mul : 1.f;
+      if constexpr (SCALE) K = __builtin_ldexpf(K, kk);
+      const float nm = fmaxf(m, bm * K);
+      const float sh = fmaxf(nm, -3.402823466e38f);
+      const float f = __builtin_amdgcn_exp2f((m - sh) * kL2E);
+      const float KL = K * kL2E;
+      const float c = nm == -INFINITY ? 0.f : -fminf(sh, 2.0e38f) * kL2E;
+      float ps = 0.f, pc = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float e = __builtin_amdgcn_exp2f(fmaf(v[i], KL, c));
+        ps += e;
+        pc = fmaf((float)((i & 3) + 8 * (i >> 2)), e, pc);
+      }
+      s = s * (double)f + (double)ps;
+      tt = tt * (double)f + (double)ub * (double)ps - (double)pc;
+      m = nm;
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int ci = (i & 3) + 8 * (i >> 2);
@@ -450,6 +491,7 @@ __device__ __forceinline__ void fold_block(const f32x16& blk, const Args& args, 
     tt = tt * (double)f + (double)ub * (double)ps - (double)pc;  // sum (ub - c_i) e
     m = nm;
     __builtin_amdgcn_sched_barrier(0);
+    }
   };
   // the first and the last block always straddle the band's ends; the middle ones only when
   // Dp < DMAX (a uniform branch: the common full-D item runs them unmasked)

@@ -405,11 +405,11 @@ __device__ __forceinline__ void sl_role(const Args& args, unsigned char* smem) {
       auto go = [&](auto scale, auto xlt) __attribute__((always_inline)) {
         constexpr bool SC = decltype(scale)::value, XL = decltype(xlt)::value;
         if constexpr (NP == 1) {
-          fused_softargmin<T, MEAN, SC, XL, false>(acc, args, pw, -p_kk, 0, rw, lr, hh);
+          fused_softargmin<T, MEAN, SC, XL, false, FoldF32>(acc, args, pw, -p_kk, 0, rw, lr, hh);
         } else {
           float m;
           double s, t;
-          fused_softargmin_state<T, MEAN, SC, XL>(acc, args, pw, -p_kk, 0, rw, lr, hh, m, s, t);
+          fused_softargmin_state<T, MEAN, SC, XL, FoldF32>(acc, args, pw, -p_kk, 0, rw, lr, hh, m, s, t);
           if (pw.pass == 0) {
             f_m = m;
             f_s = s;
