@@ -288,9 +288,8 @@ __device__ __forceinline__ int exp_of(float x) { return __builtin_amdgcn_frexp_e
 #define SMCV_SCHED_PHASE 0
 #endif
 #ifndef SMCV_FOLD_FMA
-#define SMCV_FOLD_FMA 1  // fused fold of band_sl (and band_rs at C = 16): 1/C and 2^kk folded into
-#endif                   // the exponent's FMA (0: the cells scaled one by one; cfg4 volume-free 5 %
-                         // slower, r05)
+#define SMCV_FOLD_FMA 1  // band_sl's fused fold: 1/C and 2^kk folded into the exponent's FMA (0:
+#endif                   // the cells scaled one by one; cfg4 volume-free 5 % slower, r05)
 #ifndef SMCV_SCHED_IL
 #define SMCV_SCHED_IL 0  // diagnostic: chunks of IL segments dealt round-robin to the XCD groups
 #endif                   // instead of one contiguous range each (IL a multiple of 8)

@@ -338,11 +338,7 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
     if constexpr (FUSE != 0) {
       if (p_bytes == 0) return;
       auto go = [&](auto scale, auto xlt) __attribute__((always_inline)) {
-        // C = 16 (NKS 1): band_sl's fold (the volume-kept mean at C = 16, D > 128 runs here and
-        // its volume-free call on band_sl: one disparity bit for bit); C = 64 keeps the scaled
-        // cells (the FMA form spills at NKS 4)
-        using RTF = typename std::conditional<NKS == 1, FoldF32, float>::type;
-        fused_softargmin<T, MEAN, decltype(scale)::value, decltype(xlt)::value, true, RTF>(
+        fused_softargmin<T, MEAN, decltype(scale)::value, decltype(xlt)::value>(
             acc, args, pw, -p_kk, 0, rw, lr, hh);
       };
       const bool sc = p_kk != 0, xl = pw.js < 0;

@@ -853,8 +853,10 @@ int band_sl_run(const Args& a0, int64_t N, bool mean, bool aligned4, hipStream_t
     a.pw = pw2;
     np = 2;
   }
-  // the mean with the volume kept, one channel step, D > 128: its compute wave would spill
-  if (fuse == 1 && mean && nks == 1 && a.pw > 128) return SM_OK;
+  // the mean with the volume kept, one channel step, D > 128: its compute wave would spill.  Its
+  // volume-free call stays off band_sl too: that pair (band_h2db with the volume, band_rs without)
+  // folds the scaled cells and returns one disparity bit for bit (band_sl folds with FoldF32)
+  if (mean && nks == 1 && a.pw > 128 && np == 1) return SM_OK;
   *handled = true;
   auto go = [&](auto tm, auto nk, auto npc) {
     constexpr int TM = decltype(tm)::value, NK = decltype(nk)::value, NPC = decltype(npc)::value;
