@@ -136,9 +136,12 @@ def kernel_name(cfg, pipeline, algo):
     sl_shape = f32 and cfg["C"] in (16, 64) and (64 < cfg["D"] <= 192 or (cfg["C"] == 16 and 192 < cfg["D"] <= 256))
     rs_shape = f32 and cfg["C"] in (16, 64) and cfg["D"] > 64
     if cfg["op"] in ("inner_product", "correlation") and pipeline == "separate":
+        # AUTO: the sliding-window kernel (round 6), except the correlation mean at C = 16 with
+        # one pass of more than 128 disparities (band_h2db)
+        mean16 = cfg["op"] == "correlation" and cfg["C"] == 16 and 128 < cfg["D"] <= 192
         return {"valu": "dot_volume_valu", "f32": "ip_band_f32", "mfma": "ip_band_f32",
-                "h2": "band_h2", "h2db": "band_h2db",
-                "sl": "band_sl" if sl_shape else "band_h2db"}.get(algo, "band_rs" if rs_shape else "band_h2db")
+                "h2": "band_h2", "h2db": "band_h2db", "rs": "band_rs" if rs_shape else "band_h2db",
+                }.get(algo, "band_sl" if sl_shape and not mean16 else "band_h2db")
     if pipeline == "fused":  # volume kept: FUSE 1 (one D pass); D > 192: the two kernels
         if not f32:
             return "band_h2 (fused soft-argmin, volume kept)"
@@ -555,7 +558,7 @@ def main():
         "config": {"workload": cfg["workload"], "config": a.config, "C": C, "H": H, "W": W,
                    "D": cfg["D"], **({"G": cfg["G"]} if "G" in cfg else {}),
                    "global_batch": global_batch, "pairs_per_gpu": nb,
-                   "pairs_per_launch": max(1, a.chunk or cfg["chunk"]),
+                   "pairs_per_launch": min(nb, max(1, a.chunk or cfg["chunk"])),
                    "parallelism": f"dp{world}", "algo": a.algo, "pipeline": a.pipeline,
                    "arithmetic": arithmetic(cfg, a.pipeline, a.algo)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

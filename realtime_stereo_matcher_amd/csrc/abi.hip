@@ -52,12 +52,15 @@ using namespace smcv;
 
 #ifndef SMCV_AUTO_SL
 // AUTO's volume kernel for the shapes both take: the role-split band (0) or the sliding-window
-// band (1).  The volume is bound by how HBM takes its write stream: band_rs's schedule (the eight
-// tiles of a row on eight workgroups of one XCD at once, every 3,840-B volume row written
-// together) ran 0-8 % faster than band_sl's row walk on every box measured (cfg2 32-pair launch:
-// 3,957 vs 4,263 us and 4,235 vs 4,251 us; scripts/micro/sl_pattern.hip, profiles/r05/), while
-// band_sl's lighter staging wins the fused passes (ip_h2.hip, SMCV_SL_FUSE)
-#define SMCV_AUTO_SL 0
+// band (1).  The volume is bound by how HBM takes its mixed read + write stream.  band_rs reads
+// each segment's 192-column right window again (from L2: the counted traffic stays 1.0x), and
+// those re-reads of lines a neighbouring workgroup is fetching cost 540 us of a 32-pair cfg2
+// launch's read stream (scripts/micro/mem_shapes.hip: 1,964 vs 1,422 us); band_sl reads every
+// feature column once.  Round 5's band_sl walked rows strided over the whole grid and lost on the
+// write stream; with each XCD on a contiguous eighth of the rows (SMCV_SL_MAP 1) it is the faster
+// kernel: cfg2 32 pairs 3,642-3,672 vs 3,847-3,870 us, cfg4 11,988-12,045 vs 12,375-12,448 us,
+// same process and buffers (profiles/r06/ab/), and equal on a slowly mapped volume buffer
+#define SMCV_AUTO_SL 1
 #endif
 namespace {
 // band_h2_entry's kernel choice for an algo: 6 band_sl, 5 band_rs, 2 band_h2db, 0 band_h2
@@ -95,10 +98,10 @@ extern "C" int sm_cv_inner_product_ex(const void* left, const void* right, void*
     case SM_IP_MFMA_RS:
     case SM_IP_MFMA_SL: {
       bool handled = false;
-      // AUTO / RS: fp32 aligned rows with C = 16 or 64 and 65..192 disparities per pass take the
-      // role-split band (band_rs); SL: the sliding-window band (band_sl; also C = 16 with two
-      // passes of <= 128); shapes they do not take: the double-buffered band (band_h2db) for fp32
-      // aligned rows, band_h2 for the rest
+      // AUTO / SL: fp32 aligned rows with C = 16 or 64 and 65..192 disparities per pass (and
+      // C = 16 with two passes of <= 128) take the sliding-window band (band_sl); RS: the
+      // role-split band (band_rs); shapes they do not take: the double-buffered band (band_h2db)
+      // for fp32 aligned rows, band_h2 for the rest
       const int variant = algo_variant(algo);
       int rc = band_h2_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 0,
                              stream, &handled, variant);

@@ -414,8 +414,9 @@ __device__ __forceinline__ void slow_softargmin_f32(const Args& args, const Work
 // by 2^-(kL+kR); XLT forces the cells x < d (R pad rows) to 0, as the volume has them; RT (not
 // float): the cell rounded to RT first.
 // RT = FoldFma: the fp32 cells with 1/C and 2^kk folded into the exponent's FMA (the cells stay
-// raw; their block maximum is scaled once, K > 0 keeps it the maximum).  A kernel pair whose
-// volume-kept and volume-free calls must agree bit for bit uses the same RT.
+// raw; their block maximum is scaled once, K > 0 keeps it the maximum): e = 2^(fma(x, K, -sh)
+// log2 e), two operations per cell instead of the scale, subtract and multiply.  A kernel pair
+// whose volume-kept and volume-free calls must agree bit for bit uses the same RT.
 struct FoldFma {};
 using FoldF32 = std::conditional<SMCV_FOLD_FMA != 0, FoldFma, float>::type;
 
@@ -435,7 +436,7 @@ __device__ __forceinline__ void fold_block(const f32x16& blk, const Args& args, 
     float bm = -INFINITY;
     if constexpr (std::is_same<RT, FoldFma>::value) {
       // the mean's 1/C and the scale 2^kk folded into the exponent's FMA: the cells stay raw,
-      // their maximum is scaled once (K > 0: monotonic), e = 2^(x K log2 e - max log2 e)
+      // their maximum is scaled once (K > 0: monotonic), e = 2^((x K - max) log2 e)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int ci = (i & 3) + 8 * (i >> 2);
@@ -450,12 +451,17 @@ __device__ __forceinline__ void fold_block(const f32x16& blk, const Args& args, 
       const float nm = fmaxf(m, bm * K);
       const float sh = fmaxf(nm, -3.402823466e38f);
       const float f = __builtin_amdgcn_exp2f((m - sh) * kL2E);
-      const float KL = K * kL2E;
-      const float c = nm == -INFINITY ? 0.f : -fminf(sh, 2.0e38f) * kL2E;
+      // e = 2^((x K - sh) log2 e) with x K - sh formed by one FMA (exact product, one rounding),
+      // then scaled: the exponent's error is relative to x K - sh, not to |x K|.  (Round 5's
+      // one-FMA form x (K log2 e) - sh log2 e carried an error of 2^-24 |sh| log2 e: fine for
+      // cells of O(10), but cells of 1e30 lost the maximum's own weight, NaN, and the shift
+      // needed a clamp at 2e38)  No clamp: x K - sh <= 0, and a result below
+      // -FLT_MAX rounds to -inf, e = 0.
+      const float nsh = -sh;
       float ps = 0.f, pc = 0.f;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float e = __builtin_amdgcn_exp2f(fmaf(v[i], KL, c));
+        const float e = __builtin_amdgcn_exp2f(fmaf(v[i], K, nsh) * kL2E);
         ps += e;
         pc = fmaf((float)((i & 3) + 8 * (i >> 2)), e, pc);
       }

@@ -51,6 +51,9 @@
 #ifndef SMCV_SL_SETS
 #define SMCV_SL_SETS 4  // feature-load register sets (loads issued SETS - 1 steps ahead)
 #endif
+#ifndef SMCV_SL_MAP
+#define SMCV_SL_MAP 1  // rows of a workgroup: 1 XCD-contiguous ranges, 0 strided over the grid
+#endif
 
 namespace smcv {
 namespace h2band {
@@ -125,17 +128,30 @@ __device__ __forceinline__ void sl_role(const Args& args, unsigned char* smem) {
   const int H = args.H, W = args.W, D = args.D;
   const Strides4 ls = args.ls, rs = args.rs;
 
-  // rows b, b + nwg, b + 2 nwg, ... of the (n, y) rows; segment sigma of this workgroup is row
-  // b + (sigma / tiles) nwg, tile sigma % tiles
+  // The (n, y) rows a workgroup walks: segment sigma is row rbeg + (sigma / tiles) rstep, tile
+  // sigma % tiles.  SMCV_SL_MAP 1 (with a grid of whole XCD groups): XCD group b & 7 (workgroups
+  // b and b + 8 share an XCD, as Sched assumes) owns a contiguous eighth of the rows and its
+  // workgroups take rows gi, gi + 32, ... of it, so an XCD works on ~32 neighbouring rows at a
+  // time; else rows b, b + nwg, ... (round 5).  The write stream of the first map measured 6 %
+  // faster in the memory-pattern micro (profiles/r06/memory/).
   const int bwg = blockIdx.x, nwg = gridDim.x;
   const int rows = args.nwork;
   if (bwg >= rows) return;  // the whole workgroup leaves together
-  const int nitems = ((rows - bwg + nwg - 1) / nwg) * args.tiles;
+  int rbeg = bwg, rstep = nwg, rcnt = (rows - bwg + nwg - 1) / nwg;
+  if (SMCV_SL_MAP && nwg % 8 == 0 && rows >= nwg) {  // then every group has >= nwg / 8 rows
+    const int grp = bwg & 7, gi = bwg >> 3, gsz = nwg >> 3;
+    const int q = rows / 8, r = rows % 8;
+    const int gb = grp * q + min(grp, r), gc = q + (grp < r ? 1 : 0);
+    rbeg = gb + gi;
+    rstep = gsz;
+    rcnt = (gc - gi + gsz - 1) / gsz;
+  }
+  const int nitems = rcnt * args.tiles;
   auto witem = [&](int i) -> Work {
     const unsigned ii = (unsigned)min(i, nitems - 1);
     const unsigned ri = fdiv(ii, args.fd_tiles);
     const int s = (int)(ii - ri * (unsigned)args.tiles);
-    const unsigned row = (unsigned)bwg + ri * (unsigned)nwg;
+    const unsigned row = (unsigned)rbeg + ri * (unsigned)rstep;
     const unsigned nn = fdiv(row, args.fd_h);
     Work k;
     k.n = (int)nn;

@@ -231,8 +231,13 @@ def inner_product_soft_argmin(left, right, max_disparity, mean=False, keep_volum
     (``None`` with ``keep_volume=False``: it is then never written) and the (N,1,H,W) disparity.
 
     Precision, per the reference's two calls:
-    - fp32 features: the volume and the disparity are fp32; the disparity is the soft-argmin of
-      exactly the volume returned (bit-identical between ``keep_volume`` True and False).
+    - fp32 features: the volume and the disparity are fp32.  For D <= 192 the disparity does
+      not depend on ``keep_volume`` (one kernel folds the same accumulators either way; on the
+      sliding-window kernel the fold scales the raw accumulators inside the exponent's FMA
+      rather than reading the stored cells, so it is within 1e-4 of the soft-argmin of the
+      volume returned, not bit-equal to it).  For C = 16 and D > 192 the volume-kept call runs
+      the volume kernel and the regression kernel, the volume-free call one two-pass fold: the
+      two disparities agree within 1e-4.
     - fp16 / bf16 features outside autocast: both in the feature dtype.
     - fp16 / bf16 features under ``torch.autocast`` (the reference's default eval,
       evaluate_stereo.py:48): the volume keeps the feature dtype and the disparity is fp32, the
@@ -259,21 +264,16 @@ def inner_product_soft_argmin(left, right, max_disparity, mean=False, keep_volum
     mode = 1 if mean else 0
     # autocast eval with fp16 / bf16 features: the volume keeps the feature dtype (the reference
     # assigns into zeros of left.dtype) and the soft-argmin returns fp32 -- the fused kernel's
-    # fp32-disparity mode, from the fp32 accumulators of the exact products
+    # fp32-disparity mode, which rounds each cell to the feature dtype before the fold (the
+    # volume the reference regresses); SM_FUSED_EXACT_ACC folds the fp32 accumulators instead
     f32disp = _autocast_fp32(left)
     if f32disp:
         mode |= _lib.SM_FUSED_DISP_F32
         if exact_accumulators:
             mode |= _lib.SM_FUSED_EXACT_ACC
 
-    def call(vol, disp):
+    def call(vol, disp, ws=None, nws=0):
         lib = _lib.load()
-        # the workspace serves only the volume-free fused kernel over several D passes (fp32
-        # features, or half features with fp32 disparities); the rest falls back to the
-        # two-kernel path without it
-        nws = (int(lib.sm_cv_inner_product_softargmin_workspace_bytes(n, h, w, D))
-               if vol is None and (code == _lib.SM_F32 or f32disp) else 0)
-        ws = torch.empty(nws, dtype=torch.uint8, device=dev) if nws > 0 else None
         return lib.sm_cv_inner_product_softargmin_ws(
             _ptr(left), _ptr(right), None if vol is None else _ptr(vol), _ptr(disp), code,
             n, c, h, w, D, _lib.strides_arg(left), _lib.strides_arg(right), mode,
@@ -283,7 +283,15 @@ def inner_product_soft_argmin(left, right, max_disparity, mean=False, keep_volum
         vol = torch.empty((n, D, h, w), dtype=left.dtype, device=dev) if keep else None
         disp = torch.empty((n, 1, h, w), dtype=torch.float32 if f32disp else left.dtype, device=dev)
         if disp.numel():
+            # first without a workspace: the volume-free shapes band_sl takes (C = 16, D <= 256)
+            # merge their D passes in registers and need none (the cfg4 launch used
+            # to allocate 2.6 GB it never read)
             rc = call(vol, disp)
+            if rc == _lib.SM_EUNSUPPORTED and vol is None and (code == _lib.SM_F32 or f32disp):
+                # several D passes on band_h2: their partial softmax states go to a workspace
+                nws = int(_lib.load().sm_cv_inner_product_softargmin_workspace_bytes(n, h, w, D))
+                if nws > 0:
+                    rc = call(None, disp, torch.empty(nws, dtype=torch.uint8, device=dev), nws)
             if rc == _lib.SM_EUNSUPPORTED and vol is None:
                 # not a fused shape: the two-kernel path needs the volume in HBM for a moment
                 rc = call(torch.empty((n, D, h, w), dtype=left.dtype, device=dev), disp)

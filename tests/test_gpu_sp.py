@@ -236,3 +236,69 @@ def test_rs_groupwise_16bit(shape, dt):
     assert got.shape == (n, G, h, w, D)
     want = O.groupwise(host(L), host(R), G, D)
     np.testing.assert_allclose(got, want, atol=TOL, rtol=0)
+
+
+def _softargmin_bound(vol64, eps):
+    """Rigorous per-pixel bound on the soft-argmin change under cell errors |delta_k| <= eps_k
+    (test_autocast._disp_bound's form): e^max(eps) * sum_k |k - disp| q_k (e^eps_k - 1)."""
+    q = np.exp(vol64 - vol64.max(axis=1, keepdims=True))
+    q /= q.sum(axis=1, keepdims=True)
+    k = np.arange(vol64.shape[1], dtype=np.float64).reshape(1, -1, 1, 1)
+    disp = (k * q).sum(axis=1, keepdims=True)
+    s = (np.abs(k - disp) * q * np.expm1(eps)).sum(axis=1, keepdims=True)
+    return disp, np.exp(eps.max(axis=1, keepdims=True)) * s
+
+
+@pytest.mark.parametrize("D", [160, 256])
+def test_sl_mixed_scales_c16(D):
+    """band_sl's one-channel-step (C = 16) restart path -- the range check before a
+    segment's steps, the window re-staged -- under row-to-row and pixel-to-pixel scale changes,
+    for the volume (both kernels, one and two D passes) and for the volume-free fused call
+    (D = 256: the two-pass f_m / f_s register carry across restarts, cfg4's production shape).
+    L's row scale is the inverse of R's, so the features span 1e-8 .. 1e8 while the cells stay
+    O(10) and the softmax is well conditioned.  Volume: relative 1e-5 of sum_c |L R| (the other
+    scale tests' bar).  Disparity: the fp64 soft-argmin of the oracle volume within the rigorous
+    softmax bound for cell errors of 4e-6 sum_c |L R| (the split's three dropped terms, 2^-22
+    each, and fp32 accumulation over 16 products), plus 1e-4."""
+    from realtime_stereo_matcher_amd import functional as F
+
+    rng = np.random.default_rng(D)
+    n, c, h, w = 2, 16, 6, 640
+    l, r = _feats(31, (n, c, h, w))
+    row = 10.0 ** rng.uniform(-8, 8, (n, 1, h, 1))
+    l = (l * row * 10.0 ** rng.uniform(-0.5, 0.5, (n, 1, h, w))).astype(np.float32)
+    r = (r / row * 10.0 ** rng.uniform(-0.5, 0.5, (n, 1, h, w))).astype(np.float32)
+    want = O.inner_product(l, r, D)
+    cn = _cell_norm(l, r, D)
+    for algo in ALGOS:
+        got = host(F.inner_product_volume(dev(l), dev(r), D, algo=algo))
+        err = np.abs(got - want)
+        assert (err <= 1e-5 * cn + 1e-30).all(), (algo, float((err / (1e-5 * cn + 1e-30)).max()))
+    _, disp = F.inner_product_soft_argmin(dev(l), dev(r), D, keep_volume=False)
+    ex, bound = _softargmin_bound(O._dot_volume(l.astype(np.float64), r.astype(np.float64), D),
+                                  4e-6 * O._dot_volume(np.abs(l).astype(np.float64), np.abs(r).astype(np.float64), D))
+    err = np.abs(host(disp).astype(np.float64) - ex)
+    assert (err <= bound + TOL).all(), float((err / (bound + TOL)).max())
+
+
+@pytest.mark.parametrize("D,keep", [(96, True), (96, False), (256, False)])
+def test_fused_cells_near_flt_max(D, keep):
+    """the sliding-window kernel's fused fold takes 1/C and the segment scale into the
+    exponent's FMA, whose shift is clamped at 2e38; a block whose largest cell is above that must
+    not overflow exp2.  C = 16, |L| = |R| = a with R = L, 16 a^2 = 3.2e38: every pixel's d = 0 cell
+    is 3.2e38 and the others at least 2 a^2 lower, so the soft-argmin is 0 (ties give their mean),
+    finite; the oracle's fp64 soft-argmin of the fp32 volume says the same."""
+    from realtime_stereo_matcher_amd import functional as F
+
+    rng = np.random.default_rng(7)
+    a = np.float32(np.sqrt(3.2e38 / 16))
+    l = (np.where(rng.uniform(size=(1, 16, 2, 128)) < 0.5, -a, a)).astype(np.float32)
+    r = l.copy()
+    vol, disp = F.inner_product_soft_argmin(dev(l), dev(r), D, keep_volume=keep)
+    want_vol = O.inner_product(l, r, D)
+    assert np.isfinite(want_vol).all() and want_vol.max() >= 3.0e38
+    got = host(disp)
+    assert np.isfinite(got).all()
+    np.testing.assert_allclose(got, O.softargmin(want_vol), atol=TOL, rtol=0)
+    if keep:
+        np.testing.assert_allclose(host(vol), want_vol, rtol=1e-5, atol=0)

@@ -259,3 +259,30 @@ def test_torch_port_v4_volume_loop(name):
         got = P.v4_volume_loop(torch.from_numpy(a["featL"]), torch.from_numpy(a["featR"]),
                                net.conv3d, net.volume11, 48).numpy()
     np.testing.assert_allclose(got, a["volume"], atol=1e-5, rtol=0)
+
+
+def _autocast_cases():
+    import json
+    with open(os.path.join(GOLDEN_DIR, "autocast_manifest.json")) as f:
+        return json.load(f)["cases"]
+
+
+@pytest.mark.parametrize("rec", _autocast_cases(), ids=[c["name"] for c in _autocast_cases()])
+def test_autocast_fixture(rec):
+    """The reference's fp16 eval (tests/golden/gen_autocast_golden.py): the oracle's literal form
+    (each product rounded to fp16, fp64 sum, one fp16 rounding) is within one fp16 ulp of the
+    reference's fp16 volume (its sums are fp32), and the fp64 soft-argmin of that fp16 volume is
+    the reference's fp32 disparity within the fp32 bar (its CPU fp32 softmax deviates by up to
+    8.4e-5 at disparities of ~90 px)."""
+    a = np.load(os.path.join(GOLDEN_DIR, rec["file"]))
+    D = rec["max_disparity"]
+    f = O.correlation_mean if rec["mean"] else O.inner_product
+    got = f(a["left"], a["right"], D, out_dtype="f16", literal=True).astype(np.float64)
+    ref = a["volume"].astype(np.float64)
+    ulp = np.spacing(np.abs(ref).astype(np.float16)).astype(np.float64)
+    assert (np.abs(got - ref) <= ulp).all()
+    # the literal rounding matters: the exact-product volume differs from the reference's
+    exact = f(a["left"], a["right"], D, out_dtype="f16").astype(np.float64)
+    assert (exact != ref).any()
+    np.testing.assert_allclose(O.softargmin(a["volume"].astype(np.float32)), a["disparity"],
+                               atol=TOL_F32, rtol=0)
