@@ -436,7 +436,7 @@ def cpu_baseline(cfg, a, seconds):
 
 
 # ----------------------------------------------------------------------------- PMC traffic
-EVIDENCE_ROUND = "r05"
+EVIDENCE_ROUND = "r06"
 
 
 def evidence_name(a):

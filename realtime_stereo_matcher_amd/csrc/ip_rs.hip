@@ -155,10 +155,13 @@ __device__ __forceinline__ void rs_role(const Args& args, unsigned char* smem) {
   auto load = [&](int set, const Work& k, int ks) __attribute__((always_inline)) {
     const int px = isR ? k.js + 4 * g : k.x0 + 4 * g - G::RW;
     okp[set] = active && px >= 0 && px < W;
-    if constexpr ((SMCV_RS_ABLATE & 4) && F32) {
+    if constexpr (SMCV_RS_ABLATE & 4) {
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk) {
-        sv[set][kk] = f32x4v{1.f, -1.f, 0.5f, 2.f};
+        if constexpr (F32)
+          sv[set][kk] = f32x4v{1.f, -1.f, 0.5f, 2.f};
+        else
+          sv[set][kk] = QT{0x3c003c00u, 0xbc00bc00u};
         asm volatile("" : "+v"(sv[set][kk]));
       }
       return;
@@ -764,6 +767,9 @@ int band_rs_run(const Args& a, int64_t N, bool mean, bool aligned4, hipStream_t 
 #ifndef SMCV_RS_GW
 #define SMCV_RS_GW 1  // groupwise volumes of 16-bit features on band_rs (0: band_h2)
 #endif
+#ifndef SMCV_RS_GW_SETS
+#define SMCV_RS_GW_SETS 4  // feature-load register sets of the groupwise instances (C/G >= 32)
+#endif
 // Groupwise volume (mean over C/G channels, (N, G, H, W, D) fp32) of fp16 / bf16 features on the
 // role-split kernel; *handled = false when the shape is not one it takes: 4-element aligned
 // rows, C/G a multiple of 16 (one or more 16-channel steps per group: 1, 2 or 4), one D pass of
@@ -779,7 +785,7 @@ int band_rs_gw_run(const Args& a, int64_t N, int dtype, hipStream_t st, bool* ha
   auto go = [&](auto tm, auto nk, auto ti) {
     constexpr int TM = decltype(tm)::value, NK = decltype(nk)::value;
     using TI = typename decltype(ti)::type;
-    constexpr int NS = NK == 1 ? 2 : 4;
+    constexpr int NS = NK == 1 ? 2 : SMCV_RS_GW_SETS;
     return launch_rs<true, TM, NK, NS, 0, TI, true>(a, N, st);
   };
   auto by_t = [&](auto ti) {

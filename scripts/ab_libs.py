@@ -9,7 +9,7 @@ alternate A / B as the bench's steps do.
 
 Cases: cfg2_<algo> (the 32-pair inner-product volume with algo rs / sl / auto), cfg2_fused /
 cfg2_fusednv (the fused pass with / without the volume), cfg4_<algo> (32-pair correlation
-volume D = 256), cfg4_fusednv."""
+volume D = 256), cfg4_fusednv, cfg3_auto (groupwise bf16, G = 8; use --pairs 1)."""
 import argparse
 import ctypes
 import json
@@ -55,7 +55,11 @@ def main():
     n = a.pairs
     need4 = any(c.startswith("cfg4") for c in cases)
     need2 = any(c.startswith("cfg2") for c in cases)
+    need3 = any(c.startswith("cfg3") for c in cases)
     data = {}
+    if need3:  # groupwise bf16, G = 8, (N, G, H, W, D) fp32 out
+        data["cfg3"] = (torch.randn(n, 256, 540, 960, device=dev, generator=g).bfloat16(),
+                        torch.randn(n, 256, 540, 960, device=dev, generator=g).bfloat16(), 192, 540, 960)
     if need2:
         data["cfg2"] = (torch.randn(n, 64, 540, 960, device=dev, generator=g),
                         torch.randn(n, 64, 540, 960, device=dev, generator=g), 192, 540, 960)
@@ -64,7 +68,8 @@ def main():
                         torch.randn(n, 16, 1080, 1920, device=dev, generator=g), 256, 1080, 1920)
     vols = {}
     for k, (L, R, D, h, w) in data.items():
-        vols[k] = (torch.empty(n, D, h, w, device=dev), torch.empty(n, D, h, w, device=dev))
+        G = 8 if k == "cfg3" else 1
+        vols[k] = (torch.empty(n, G * D, h, w, device=dev), torch.empty(n, G * D, h, w, device=dev))
     disp = {k: torch.empty(n, 1, v[3], v[4], device=dev) for k, v in data.items()}
 
     def launch(lib, case, vol):
@@ -73,7 +78,10 @@ def main():
         c = L.shape[1]
         ls, rs = _lib.strides_arg(L), _lib.strides_arg(R)
         mean = cfg == "cfg4"
-        if kind.startswith("fused"):
+        if cfg == "cfg3":
+            rc = lib.sm_cv_groupwise(L.data_ptr(), R.data_ptr(), vol.data_ptr(), _lib.SM_BF16, n, c, h, w, D, 8,
+                                     ls, rs, st.cuda_stream)
+        elif kind.startswith("fused"):
             keep = kind == "fused"
             rc = lib.sm_cv_inner_product_softargmin_ws(L.data_ptr(), R.data_ptr(), vol.data_ptr() if keep else None,
                                                        disp[cfg].data_ptr(), _lib.SM_F32, n, c, h, w, D, ls, rs,
@@ -95,7 +103,7 @@ def main():
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) * 1e3
 
-    alg = {"cfg2": 663552000, "cfg4": 2388787200}
+    alg = {"cfg2": 663552000, "cfg4": 2388787200, "cfg3": 3715891200}
     for rnd in range(a.rounds):
         for case in cases:
             for name, lib in libs:

@@ -11,7 +11,8 @@ Per configuration NAME it writes profiles/ROUND/NAME/:
                       (FETCH_SIZE KiB x2 on gfx950 for 16-B/lane streaming reads, WRITE_SIZE KiB
                       exact), plus (cfg3) the MFMA busy fraction from SQ_VALU_MFMA_BUSY_CYCLES
 and profiles/ROUND/summary.json with one row per configuration (bench kernel time vs the
-rocprofv3 average of the dominant kernel, algorithmic vs counted bytes).
+rocprofv3 average of the dominant kernel -- the profiled process's own HIP-event average beside
+it, profiled_bench_avg_kernel_us -- algorithmic vs counted bytes).
 """
 import csv
 import glob
@@ -87,6 +88,15 @@ def main():
             top = max(rows, key=lambda r: float(r["TotalDurationNs"]))
             row["rocprof_top_kernel"] = top["Name"]
             row["rocprof_avg_us"] = float(top["AverageNs"]) / 1e3
+            # the profiled process's own bench line (kt.json): the same launches, timed by the
+            # bench's HIP events and by the kernel trace; a separate process may draw differently
+            # mapped volume buffers (profiles/r05/placement/), so this is the like-for-like pair
+            kt = os.path.join(d, "kt.json")
+            if os.path.exists(kt) and os.path.getsize(kt) > 0:
+                with open(kt) as f:
+                    ktb = json.loads(f.read().strip().splitlines()[-1])
+                row["profiled_bench_avg_kernel_us"] = ktb["roofline"]["avg_kernel_us"]
+                row["profiled_bench_value"] = ktb["value"]
         pmc = {"correction": "hbm_bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 (gfx950)", "kernels": {}}
         fp, wp = find(os.path.join(d, "FETCH_SIZE"), "*counter_collection.csv"), find(os.path.join(d, "WRITE_SIZE"), "*counter_collection.csv")
         if fp and wp:

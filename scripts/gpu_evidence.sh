@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round evidence for every bench configuration: the bench line, a rocprofv3 kernel-trace/stats
-# profile of the same command, and the HBM counter passes (FETCH_SIZE, WRITE_SIZE: one --pmc per
+# profile of the same command (the same steps and warm-up: the bench's steps alternate two volume
+# buffers, which some boxes map at different speeds, so both runs see the same alternation), and the HBM counter passes (FETCH_SIZE, WRITE_SIZE: one --pmc per
 # run, kernel trace only); for the groupwise MFMA path also SQ_VALU_MFMA_BUSY_CYCLES with
 # SQ_BUSY_CYCLES / GRBM_GUI_ACTIVE.  Fold the result into profiles/ with scripts/evidence_summary.py.
 #   bash scripts/gpu_evidence.sh TAG ["name:bench args" ...]
@@ -19,7 +20,7 @@ for spec in "${SPECS[@]}"; do
   echo "== $n: $args"
   timeout -k 10 300 python bench.py $args > "$D/bench.json" 2> "$D/bench.err" || { echo "bench $n failed"; exit 2; }
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$D/kt" -o run --output-format csv -- \
-    python3 bench.py --steps 10 --warmup 3 --cpu-baseline-seconds 0 --no-check $args > "$D/kt.json" 2> "$D/kt.err" || { echo "kt $n failed"; exit 3; }
+    python3 bench.py --cpu-baseline-seconds 0 --no-check $args > "$D/kt.json" 2> "$D/kt.err" || { echo "kt $n failed"; exit 3; }
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d "$D/$c" -o run -- \
       python3 bench.py --steps 3 --warmup 1 --cpu-baseline-seconds 0 --no-check $args > "$D/$c.log" 2>&1 || { echo "pmc $c $n failed"; exit 4; }

@@ -24,7 +24,10 @@ CASES = [("w px128 nt (band_rs)", 0, "w"), ("w px256 nt", 1, "w"), ("w px512 nt"
          ("rw units +win (band_rs)", 30, "rw"), ("rw units", 31, "rw"), ("rw rowwalk xcd +win", 32, "rw"),
          ("rw rowwalk xcd (band_sl)", 33, "rw"), ("band_sl", "sl", "rw"),
          ("w rowwalk xcd stagger wg", 25, "w"), ("w rowwalk xcd stagger wg+unit", 26, "w"),
-         ("w units stagger wg", 27, "w")]
+         ("w units stagger wg", 27, "w"),
+         ("gw w 4 waves nt (band_rs GW)", 40, "gw"), ("gw w 4 waves plain", 41, "gw"),
+         ("gw w 8 waves nt", 42, "gw"), ("gw w 8 waves plain", 43, "gw"),
+         ("gw w rowwalk 4 waves nt", 44, "gw"), ("gw w rowwalk 4 waves plain", 45, "gw")]
 
 
 def main():
@@ -32,6 +35,7 @@ def main():
     ap.add_argument("--pairs", type=int, default=32)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--only", default="", help="comma-separated variant numbers")
+    ap.add_argument("--gw-pairs", type=int, default=0, help="groupwise write cases only, with N pairs")
     a = ap.parse_args()
     n, c, h, w, D = a.pairs, 64, 540, 960, 192
     dev = torch.device("cuda:0")
@@ -44,7 +48,10 @@ def main():
     micro.mem_run.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 3 + [ctypes.c_int, ctypes.c_void_p]
     lib = _lib.load()
     st = torch.cuda.current_stream()
-    nbytes = {"r": 2 * c * h * w * 4, "w": D * h * w * 4, "rw": 2 * c * h * w * 4 + D * h * w * 4}
+    nbytes = {"r": 2 * c * h * w * 4, "w": D * h * w * 4, "rw": 2 * c * h * w * 4 + D * h * w * 4,
+              "gw": 8 * D * h * w * 4}
+    if a.gw_pairs:  # the groupwise writes need G x the volume: their own buffers (A, B per cfg3 pair)
+        n = a.gw_pairs
 
     def timed(variant, vol):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -212,6 +212,33 @@ __global__ __launch_bounds__(512) void rw(const float* __restrict__ L, const flo
   if (acc.x == 12345.f) out[threadIdx.x] = acc.y;
 }
 
+// cfg3's groupwise output (N, G, H, W, D) fp32, G = 8, D = 192: a unit (n, g, y, 128-px tile)
+// is 128 pixel records of 768 B, 96 KB contiguous; NW waves of the workgroup write it, 1 KiB per
+// store instruction (band_rs GW: 4 compute waves, 24 pieces each).  ORDER 0: units in band_rs's
+// XCD-contiguous order; 1: the units of one (n, g, y) row walked by one workgroup (row walk)
+template <int NW, bool PLAIN, int ORDER>
+__global__ __launch_bounds__(512) void wr_gw(float* __restrict__ out, int np) {
+  constexpr int G = 8, TPR = 8;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (wave >= NW) return;
+  int ub, us, uc;
+  // rows here are (n, g, y): np G H of them
+  sched_o<ORDER, TPR>(np * G, ub, us, uc);
+  const f4 v = {1.f, 2.f, 3.f, (float)lane};
+  for (int k = 0; k < uc; ++k) {
+    int row, tile;
+    unit_rc<ORDER, TPR>(ub, us, k, row, tile);
+    const int x0 = tile * 128;
+    const int npx = min(128, W - x0);
+    float* ob = out + ((size_t)row * W + x0) * D;  // row = (n G + g) H + y
+    const int nb = npx * D * 4 / 1024;               // 1-KiB pieces of the unit
+    for (int i = wave; i < nb; i += NW) {
+      f4* p = reinterpret_cast<f4*>(ob + (size_t)i * 256 + 4 * lane);
+      if (PLAIN) *p = v; else __builtin_nontemporal_store(v, p);
+    }
+  }
+}
+
 template <typename K, typename... A>
 int launch(K k, hipStream_t st, A... a) {
   hipLaunchKernelGGL(k, dim3(256), dim3(512), 0, st, a...);
@@ -244,6 +271,12 @@ extern "C" int mem_run(int variant, const float* L, const float* R, float* out, 
     case 25: return launch(wr<128, false, 1, 1>, st, out, np);
     case 26: return launch(wr<128, false, 1, 2>, st, out, np);
     case 27: return launch(wr<128, false, 0, 1>, st, out, np);
+    case 40: return launch(wr_gw<4, false, 0>, st, out, np);
+    case 41: return launch(wr_gw<4, true, 0>, st, out, np);
+    case 42: return launch(wr_gw<8, false, 0>, st, out, np);
+    case 43: return launch(wr_gw<8, true, 0>, st, out, np);
+    case 44: return launch(wr_gw<4, false, 1>, st, out, np);
+    case 45: return launch(wr_gw<4, true, 1>, st, out, np);
     case 30: return launch(rw<0, true>, st, L, R, out, np);
     case 31: return launch(rw<0, false>, st, L, R, out, np);
     case 32: return launch(rw<1, true>, st, L, R, out, np);

@@ -55,11 +55,10 @@ def test_evidence_summary_consistent():
     with open(path) as f:
         summary = json.load(f)
     for name, row in summary.items():
-        # the rocprofv3 average of the dominant kernel agrees with the bench's HIP events.  The
-        # 4-pair cfg4 launch (1.6 ms) is the exception the record states: its profiled process
-        # alternated a slow and a fast volume buffer (1,549-1,576 / 1,946-1,993 us per launch,
-        # profiles/r05/placement/README.md), the bench's process did not
-        tol = 0.2 if name == "cfg4_b4" else 0.1
-        assert abs(row["rocprof_avg_us"] / row["bench_avg_kernel_us"] - 1) < tol, name
+        # the rocprofv3 average of the dominant kernel agrees with the HIP events of the same
+        # profiled process (round 6 records it; earlier rounds compared with the separate bench
+        # process, whose volume buffers may be mapped at another speed, profiles/r05/placement/)
+        bench_us = row.get("profiled_bench_avg_kernel_us", row["bench_avg_kernel_us"])
+        assert abs(row["rocprof_avg_us"] / bench_us - 1) < 0.1, name
         if "mfma_busy_frac" in row:
             assert 0.0 < row["mfma_busy_frac"] < 1.0
