@@ -16,6 +16,10 @@
  *   - Outputs are dense, contiguous, in the layout stated per function.
  *   - dtype codes: SM_F32, SM_F16, SM_BF16 (the output dtype equals the input dtype
  *     unless the function says otherwise).  Accumulation is always fp32 or wider.
+ *     SM_F64 (round 6): the cost volumes (a-1 .. a-6, computed in fp64; groupwise into its
+ *     float32 volume), the regressions (a-7, a-8, fp64 arithmetic) and the fused call's
+ *     two-kernel path, as torch computes an fp64 input; the warp and the V4 volume are float32
+ *     only (SM_EDTYPE).
  *   - Return 0 on success, a negative SM_E* code on failure; sm_last_error() then
  *     returns a thread-local, human-readable message.
  */
@@ -28,7 +32,7 @@
 extern "C" {
 #endif
 
-enum sm_dtype { SM_F32 = 0, SM_F16 = 1, SM_BF16 = 2 };
+enum sm_dtype { SM_F32 = 0, SM_F16 = 1, SM_BF16 = 2, SM_F64 = 3 };
 enum sm_status {
   SM_OK = 0,
   SM_EINVAL = -1,
@@ -78,13 +82,16 @@ enum sm_ip_algo {
   SM_IP_MFMA_RS = 11,    /* role-split band kernel: per SIMD a compute wave (MFMAs, shear ring,
                             volume stores) and a memory wave (feature loads and staging); fp32,
                             aligned rows, C = 16 or 64, D in 65..192 per pass; other shapes:
-                            MFMA_H2DB.  AUTO's choice for the volume on the shapes it takes */
+                            MFMA_H2DB.  AUTO's volume kernel in rounds 4-5; since round 6 AUTO
+                            takes MFMA_SL, and MFMA_RS keeps the groupwise 16-bit volumes */
   SM_IP_MFMA_SL = 12     /* sliding-window role-split band kernel: a workgroup walks whole rows
                             and keeps the right window of all channels in LDS, so a 128-pixel
                             segment stages only its own 128 left and 128 new right columns;
                             shapes of MFMA_RS plus (C = 16) two passes of <= 128 disparities
-                            (D = 256); others: MFMA_H2DB.  The fused volume + soft-argmin calls
-                            (sm_cv_inner_product_softargmin*) take it for fp32 features */
+                            (D = 256); others: MFMA_H2DB.  Each XCD walks a contiguous eighth of
+                            the rows.  AUTO's volume kernel for fp32 features since round 6, and
+                            the fused volume + soft-argmin calls (sm_cv_inner_product_softargmin*)
+                            take it for fp32 features */
 };
 
 /* Library version (major*10000 + minor*100 + patch). */

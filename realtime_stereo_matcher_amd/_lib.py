@@ -10,7 +10,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("STEREOCV_LIB", os.path.join(_HERE, "libstereocv.so"))
 
-SM_F32, SM_F16, SM_BF16 = 0, 1, 2
+SM_F32, SM_F16, SM_BF16, SM_F64 = 0, 1, 2, 3
 SM_OK, SM_EINVAL, SM_EDTYPE, SM_ELAUNCH, SM_EUNSUPPORTED = 0, -1, -2, -3, -4
 SM_ARGMIN, SM_ARGMAX = 0, 1
 SM_REGRESS_SOFTMAX, SM_REGRESS_PRESOFTMAXED, SM_REGRESS_OUT_F32 = 0, 1, 2

@@ -82,6 +82,13 @@ extern "C" int sm_cv_inner_product_ex(const void* left, const void* right, void*
                                       const int64_t* l_strides, const int64_t* r_strides,
                                       int algo, void* stream) {
   SM_ENTRY_BEGIN
+  if (dtype == SM_F64) {  // fp64 features: fp64 products and sums whatever the algo (f64.hip)
+    if (algo != SM_IP_AUTO && algo != SM_IP_VALU && algo != SM_IP_MFMA_F32 && algo != SM_IP_MFMA_H2 &&
+        algo != SM_IP_MFMA_H2DB && algo != SM_IP_MFMA_RS && algo != SM_IP_MFMA_SL)
+      return fail(SM_EINVAL, "unknown inner-product algo");
+    return dot_volume_valu_entry(left, right, out, dtype, N, C, H, W, D, 1, l_strides, r_strides,
+                                 0, stream);
+  }
   switch (algo) {
     case SM_IP_MFMA_F32: {
       // exact fp32 MFMA band kernel; shapes the DMA path cannot take go to the VALU kernel
@@ -132,6 +139,7 @@ extern "C" int sm_cv_correlation_mean_ex(const void* left, const void* right, vo
   SM_ENTRY_BEGIN
   bool handled = false;
   int rc = SM_OK;
+  if (dtype == SM_F64) algo = SM_IP_VALU;  // fp64: the fp64 kernel below (f64.hip)
   switch (algo) {
     case SM_IP_MFMA_F32:
       rc = band_f32_entry(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, 1,
@@ -170,6 +178,9 @@ extern "C" int sm_cv_groupwise(const void* left, const void* right, float* out, 
                                const int64_t* l_strides, const int64_t* r_strides,
                                void* stream) {
   SM_ENTRY_BEGIN
+  if (dtype == SM_F64)  // fp64 means rounded once into the float32 volume (f64.hip)
+    return dot_volume_valu_entry(left, right, out, dtype, N, C, H, W, D, G, l_strides, r_strides,
+                                 2, stream);
   // the MFMA band kernel (D-innermost epilogue); shapes it does not take: the VALU kernel
   bool handled = false;
   int rc = band_h2_groupwise_entry(left, right, out, dtype, N, C, H, W, D, G, l_strides,
@@ -188,7 +199,7 @@ int fused_softargmin(const void* left, const void* right, void* out_volume, void
     return fail(SM_EINVAL,
                 "mode must be 0 (sum) or 1 (mean), optionally | SM_FUSED_DISP_F32 | SM_FUSED_EXACT_ACC");
   const bool f32disp = (mode & SM_FUSED_DISP_F32) != 0;
-  if (!valid_dtype(dtype)) return fail(SM_EDTYPE, "unsupported dtype code");
+  if (!valid_dtype(dtype) && dtype != SM_F64) return fail(SM_EDTYPE, "unsupported dtype code");
   if (ws_bytes < 0) return fail(SM_EINVAL, "negative workspace size");
   if (D == 0 && N * H * W > 0) {  // softmax over an empty axis: the weighted sum is 0
     if (disparity == nullptr) return fail(SM_EINVAL, "null disparity pointer");
@@ -198,10 +209,13 @@ int fused_softargmin(const void* left, const void* right, void* out_volume, void
     return e == hipSuccess ? SM_OK : fail(SM_ELAUNCH, hipGetErrorString(e));
   }
   bool handled = false;
-  int rc = band_h2_fused_entry(left, right, out_volume, static_cast<float*>(disparity), dtype, N,
-                               C, H, W, D, l_strides, r_strides, mode, stream, &handled,
-                               workspace, ws_bytes);
-  if (handled || rc != SM_OK) return rc;
+  int rc = SM_OK;
+  if (dtype != SM_F64) {  // fp64: the volume and the fp64 regression below
+    rc = band_h2_fused_entry(left, right, out_volume, static_cast<float*>(disparity), dtype, N, C,
+                             H, W, D, l_strides, r_strides, mode, stream, &handled, workspace,
+                             ws_bytes);
+    if (handled || rc != SM_OK) return rc;
+  }
   if (out_volume == nullptr)
     return fail(SM_EUNSUPPORTED,
                 "fused cost volume + soft-argmin needs fp32 features (W >= 4) and D <= 192, or a "

@@ -52,8 +52,17 @@ template <> struct io<bf16_t> {
 template <typename T> __device__ __forceinline__ float to_f(T v) { return io<T>::to_f(v); }
 template <typename T> __device__ __forceinline__ T from_f(float v) { return io<T>::from_f(v); }
 
-inline int elem_size(int dtype) { return dtype == SM_F32 ? 4 : 2; }
+inline int elem_size(int dtype) { return dtype == SM_F64 ? 8 : dtype == SM_F32 ? 4 : 2; }
 inline bool valid_dtype(int dtype) { return dtype == SM_F32 || dtype == SM_F16 || dtype == SM_BF16; }
+
+// float64 (f64.hip; the copies in cv_copy.hip)
+int f64_dot_entry(const void* left, const void* right, void* out, int64_t N, int64_t C, int64_t H,
+                  int64_t W, int64_t D, int64_t G, const int64_t* l_strides,
+                  const int64_t* r_strides, int mode, void* stream);
+int f64_softargmin_entry(const void* volume, void* out, int64_t N, int64_t D, int64_t H, int64_t W,
+                         int flags, const int64_t* vol_strides, void* stream);
+int f64_argext_entry(const void* volume, int64_t* out, int64_t N, int64_t D, int64_t H, int64_t W,
+                     int mode, const int64_t* vol_strides, void* stream);
 
 // ------------------------------------------------------------------------------- views
 // Element strides of an (N, C, H, W) feature map; W stride is 1 by contract.

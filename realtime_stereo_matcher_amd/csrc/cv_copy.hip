@@ -23,6 +23,7 @@ constexpr int kRowMax = 8192;  // elements of one staged row (fp32: 32 KiB per r
 template <int BYTES> struct raw;
 template <> struct raw<2> { using type = uint16_t; };
 template <> struct raw<4> { using type = uint32_t; };
+template <> struct raw<8> { using type = uint64_t; };
 
 // 16-byte vector of raw elements.
 template <typename U> struct vec16 {
@@ -143,6 +144,15 @@ __global__ __launch_bounds__(kThreads) void interweave_kernel(const U* __restric
   }
 }
 
+// one subtraction in the input dtype (fp64 natively; the 16-bit types through fp32, exact
+// before the one rounding), and the difference volume's 1.0 fill
+template <typename T> __device__ __forceinline__ T diff(T a, T b) { return from_f<T>(to_f(a) - to_f(b)); }
+template <> __device__ __forceinline__ double diff<double>(double a, double b) { return a - b; }
+template <typename T> __device__ __forceinline__ T one() { return from_f<T>(1.f); }
+template <> __device__ __forceinline__ double one<double>() { return 1.0; }
+template <typename T> __device__ __forceinline__ T zero() { return from_f<T>(0.f); }
+template <> __device__ __forceinline__ double zero<double>() { return 0.0; }
+
 // ------------------------------------------- shifted interweave (N,2C,D,H,W) / diff (N,C,D,H,W)
 // MODE 0: shifted interweave (raw copy, 0 fill); MODE 1: L - R(x-d) with 1.0 fill.
 template <typename T, int MODE, bool VEC, bool STAGED>
@@ -179,11 +189,11 @@ __global__ __launch_bounds__(kThreads) void shifted_rows_kernel(const T* __restr
   if (MODE == 0) {
     base0 = out + ((size_t)n * 2 * C + 2 * c) * D * plane + (size_t)y * W;
     base1 = out + ((size_t)n * 2 * C + 2 * c + 1) * D * plane + (size_t)y * W;
-    zero_or_one = from_f<T>(0.f);
+    zero_or_one = zero<T>();
   } else {
     base0 = out + ((size_t)n * C + c) * D * plane + (size_t)y * W;
     base1 = base0;
-    zero_or_one = from_f<T>(1.f);
+    zero_or_one = one<T>();
   }
   constexpr int NV = 16 / sizeof(T);
   for (int d = 0; d < D; ++d) {
@@ -204,7 +214,7 @@ __global__ __launch_bounds__(kThreads) void shifted_rows_kernel(const T* __restr
             a[k] = ok ? lv : zero_or_one;
             b[k] = ok ? rv : zero_or_one;
           } else {
-            a[k] = ok ? from_f<T>(to_f(lv) - to_f(rv)) : zero_or_one;
+            a[k] = ok ? diff(lv, rv) : zero_or_one;
           }
         }
         using V = typename raw<sizeof(T)>::type;
@@ -220,7 +230,7 @@ __global__ __launch_bounds__(kThreads) void shifted_rows_kernel(const T* __restr
           o0[x] = ok ? lv : zero_or_one;
           o1[x] = ok ? rv : zero_or_one;
         } else {
-          o0[x] = ok ? from_f<T>(to_f(lv) - to_f(rv)) : zero_or_one;
+          o0[x] = ok ? diff(lv, rv) : zero_or_one;
         }
       }
     }
@@ -269,7 +279,7 @@ int concat_entry(const void* left, const void* right, void* out, int dtype, int6
       hipLaunchKernelGGL((concat_kernel<U, false, false>), grid, dim3(kThreads), shm, st, l, r, \
                          o, (int)C, (int)H, (int)W, (int)D, ls, rs, -1);                       \
   } while (0)
-  if (es == 4) SM_CONCAT_LAUNCH(uint32_t); else SM_CONCAT_LAUNCH(uint16_t);
+  if (es == 8) SM_CONCAT_LAUNCH(uint64_t); else if (es == 4) SM_CONCAT_LAUNCH(uint32_t); else SM_CONCAT_LAUNCH(uint16_t);
 #undef SM_CONCAT_LAUNCH
   return check_launch("concat_kernel");
 }
@@ -302,7 +312,7 @@ int interweave_entry(const void* left, const void* right, void* out, int dtype, 
       hipLaunchKernelGGL((interweave_kernel<U, false>), grid, dim3(kThreads), 0, st, l, r, o,  \
                          (int)C, (int)H, (int)W, ls, rs);                                      \
   } while (0)
-  if (es == 4) SM_IW_LAUNCH(uint32_t); else SM_IW_LAUNCH(uint16_t);
+  if (es == 8) SM_IW_LAUNCH(uint64_t); else if (es == 4) SM_IW_LAUNCH(uint32_t); else SM_IW_LAUNCH(uint16_t);
 #undef SM_IW_LAUNCH
   return check_launch("interweave_kernel");
 }
@@ -346,9 +356,11 @@ int shifted_entry(const void* left, const void* right, void* out, int dtype, int
   hipStream_t st = as_stream(stream);
   if (mode == 0) {
     // raw-bit copy: fp16 and bf16 share one 16-bit instantiation
+    if (dtype == SM_F64) return launch_shifted<double, 0>(left, right, out, N, C, H, W, D, ls, rs, st);
     if (dtype == SM_F32) return launch_shifted<float, 0>(left, right, out, N, C, H, W, D, ls, rs, st);
     return launch_shifted<__half, 0>(left, right, out, N, C, H, W, D, ls, rs, st);
   }
+  if (dtype == SM_F64) return launch_shifted<double, 1>(left, right, out, N, C, H, W, D, ls, rs, st);
   SM_DISPATCH_DTYPE(dtype, T,
                     return launch_shifted<T, 1>(left, right, out, N, C, H, W, D, ls, rs, st));
   return SM_OK;

@@ -154,7 +154,7 @@ int launch_dot(const void* l, const void* r, void* o, int64_t N, int64_t C, int6
 int check_dot_args(const void* left, const void* right, const void* out, int dtype, int64_t N,
                    int64_t C, int64_t H, int64_t W, int64_t D, const int64_t* l_strides,
                    const int64_t* r_strides, Strides4* ls, Strides4* rs) {
-  if (!valid_dtype(dtype)) return fail(SM_EDTYPE, "unsupported dtype code");
+  if (!valid_dtype(dtype) && dtype != SM_F64) return fail(SM_EDTYPE, "unsupported dtype code");
   if (N < 0 || C < 0 || H < 0 || W < 0 || D < 0) return fail(SM_EINVAL, "negative size");
   if (H > 65535 || W > (1 << 30) || D > (1 << 20) || C > (1 << 24))
     return fail(SM_EINVAL, "size out of supported range (H <= 65535)");
@@ -174,6 +174,8 @@ int dot_volume_valu_entry(const void* left, const void* right, void* out, int dt
   // mode 0: inner product (sum, NDHW, out dtype = in dtype)
   // mode 1: correlation mean (NDHW, out dtype = in dtype)
   // mode 2: groupwise mean (NGHWD, fp32 out)
+  if (dtype == SM_F64)  // fp64 products and sums (f64.hip)
+    return f64_dot_entry(left, right, out, N, C, H, W, D, G, l_strides, r_strides, mode, stream);
   Strides4 ls, rs;
   int rc = check_dot_args(left, right, out, dtype, N, C, H, W, D, l_strides, r_strides, &ls, &rs);
   if (rc) return rc;

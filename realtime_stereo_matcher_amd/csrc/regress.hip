@@ -424,6 +424,7 @@ inline void flatten_plane(const VolView& vs, int64_t* H, int64_t* W) {
 
 int softargmin_entry(const void* volume, void* out, int dtype, int64_t N, int64_t D, int64_t H,
                      int64_t W, int flags, const int64_t* vol_strides, void* stream) {
+  if (dtype == SM_F64) return f64_softargmin_entry(volume, out, N, D, H, W, flags, vol_strides, stream);
   VolView vs;
   int rc = check_vol(volume, out, dtype, N, D, H, W, vol_strides, &vs);
   if (rc) return rc;
@@ -490,6 +491,7 @@ int softargmin_entry(const void* volume, void* out, int dtype, int64_t N, int64_
 
 int argext_entry(const void* volume, int64_t* out, int dtype, int64_t N, int64_t D, int64_t H,
                  int64_t W, int mode, const int64_t* vol_strides, void* stream) {
+  if (dtype == SM_F64) return f64_argext_entry(volume, out, N, D, H, W, mode, vol_strides, stream);
   VolView vs;
   int rc = check_vol(volume, out, dtype, N, D, H, W, vol_strides, &vs);
   if (rc) return rc;

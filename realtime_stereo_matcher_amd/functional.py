@@ -28,7 +28,11 @@ import torch
 
 from . import _lib
 
-_DTYPES = {torch.float32: _lib.SM_F32, torch.float16: _lib.SM_F16, torch.bfloat16: _lib.SM_BF16}
+# float64 (round 6): the cost volumes and the regressions in fp64 (csrc/f64.hip), as torch
+# computes an fp64 input; the warp and the V4 volume stay float32 / 16-bit
+_DTYPES = {torch.float32: _lib.SM_F32, torch.float16: _lib.SM_F16, torch.bfloat16: _lib.SM_BF16,
+           torch.float64: _lib.SM_F64}
+_WARP_DTYPES = (torch.float32, torch.float16, torch.bfloat16)
 _ALGOS = {"auto": _lib.SM_IP_AUTO, "valu": _lib.SM_IP_VALU, "mfma": _lib.SM_IP_MFMA_F32,
           "f32": _lib.SM_IP_MFMA_F32, "h2": _lib.SM_IP_MFMA_H2, "h2db": _lib.SM_IP_MFMA_H2DB,
           "rs": _lib.SM_IP_MFMA_RS, "sl": _lib.SM_IP_MFMA_SL}
@@ -61,7 +65,7 @@ def _device_check(*ts):
 def _dtype_code(t):
     code = _DTYPES.get(t.dtype)
     if code is None:
-        raise TypeError(f"unsupported dtype {t.dtype}; expected float32, float16 or bfloat16")
+        raise TypeError(f"unsupported dtype {t.dtype}; expected float32, float16, bfloat16 or float64")
     return code
 
 
@@ -552,7 +556,7 @@ def warp_by_flow_map(image, flow):
     if image.shape[0] != n:
         raise RuntimeError(f"warp_by_flow_map: image batch {image.shape[0]} != flow batch {n}")
     for t in (image, flow):
-        if t.dtype not in _DTYPES:
+        if t.dtype not in _WARP_DTYPES:
             raise TypeError(f"warp_by_flow_map: unsupported dtype {t.dtype}; expected float32, "
                             "float16 or bfloat16")
     dev = _device_check(image, flow)

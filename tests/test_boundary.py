@@ -113,7 +113,11 @@ def test_reference_error_conventions(manifest):
     assert manifest["shape_mismatch_raises"] == "RuntimeError"
     with pytest.raises(RuntimeError, match="shape mismatch"):
         TorchInnerProductCost(3)(torch.zeros(1, 4, 2, 8), torch.zeros(1, 5, 2, 8))
-    with pytest.raises(TypeError):
+    with pytest.raises(TypeError):  # integer features: no floating dtype the engine takes
+        TorchInnerProductCost(3)(torch.zeros(1, 4, 2, 8, dtype=torch.int32),
+                                 torch.zeros(1, 4, 2, 8, dtype=torch.int32))
+    # float64 is accepted (round 6) and, on the CPU, refused as any CPU tensor is
+    with pytest.raises(RuntimeError, match="HIP devices only"):
         TorchInnerProductCost(3)(torch.zeros(1, 4, 2, 8, dtype=torch.float64),
                                  torch.zeros(1, 4, 2, 8, dtype=torch.float64))
 

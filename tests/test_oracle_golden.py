@@ -286,3 +286,44 @@ def test_autocast_fixture(rec):
     assert (exact != ref).any()
     np.testing.assert_allclose(O.softargmin(a["volume"].astype(np.float32)), a["disparity"],
                                atol=TOL_F32, rtol=0)
+
+
+def _f64_cases():
+    import json
+    with open(os.path.join(GOLDEN_DIR, "f64_manifest.json")) as f:
+        return json.load(f)["cases"]
+
+
+@pytest.mark.parametrize("rec", _f64_cases(), ids=[c["name"] for c in _f64_cases()])
+def test_f64_fixture(rec):
+    """The oracle's fp64 restatement against the reference's fp64 outputs
+    (tests/golden/gen_f64_golden.py): sums within 1e-12 of sum |L R|, copies bit-exact."""
+    a = np.load(os.path.join(GOLDEN_DIR, rec["file"]))
+    p, op, want = rec["params"], rec["op"], a["out"]
+    if op in ("inner_product", "correlation"):
+        D = p.get("max_disparity", p.get("max_disp"))
+        got = O._dot_volume(a["left"], a["right"], D) / (a["left"].shape[1] if op == "correlation" else 1)
+        norm = O._dot_volume(np.abs(a["left"]), np.abs(a["right"]), D)
+        assert (np.abs(got - want) <= 1e-12 * (norm + 1)).all()
+    elif op == "groupwise":
+        got = O.groupwise(a["left"], a["right"], p["n_groups"], p["max_disparity"])
+        np.testing.assert_allclose(got, want, rtol=2 ** -23, atol=1e-30)
+    elif op == "concat":
+        np.testing.assert_array_equal(O.concatenate(a["left"], a["right"], p["max_disparity"]), want)
+    elif op == "interweave":
+        np.testing.assert_array_equal(O.interweave(a["left"], a["right"]), want)
+    elif op == "diff_volume":
+        np.testing.assert_array_equal(O.diff_volume(a["left"], a["right"], p["max_disp"]), want)
+    elif op == "argmax":
+        np.testing.assert_array_equal(O.argext(a["volume"], "max"), want)
+    elif op in ("softargmin", "regression_presoftmax"):
+        v = a["volume"]
+        d = np.arange(v.shape[1], dtype=np.float64).reshape(1, -1, 1, 1)
+        if op == "softargmin":
+            q = np.exp(v - v.max(axis=1, keepdims=True))
+            got = (q * d).sum(axis=1, keepdims=True) / q.sum(axis=1, keepdims=True)
+        else:
+            got = (v * d).sum(axis=1)
+        np.testing.assert_allclose(got, want, atol=1e-12, rtol=0)
+    else:
+        raise AssertionError(op)
