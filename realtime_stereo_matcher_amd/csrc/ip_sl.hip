@@ -54,6 +54,9 @@
 #ifndef SMCV_SL_MAP
 #define SMCV_SL_MAP 1  // rows of a workgroup: 1 XCD-contiguous ranges, 0 strided over the grid
 #endif
+#ifndef SMCV_SL_FOLD_IL
+#define SMCV_SL_FOLD_IL 0  // 1: fold block t right before its MFMAs (measured 4-7 % slower, r6q); 0: all first
+#endif
 
 namespace smcv {
 namespace h2band {
@@ -412,6 +415,40 @@ __device__ __forceinline__ void sl_role(const Args& args, unsigned char* smem) {
     p_ob = static_cast<float*>(args.out) +
            (((int64_t)k.n * D + k.dp) * plane_stride + (int64_t)k.y * W + k.x0 + 32 * rw);
   };
+  // the previous pass's fold finished: the lane pair merged, then the disparity stored (one D
+  // pass) or pass 0's state kept in registers for pass 1 (two passes)
+  [[maybe_unused]] float fm = -INFINITY;
+  [[maybe_unused]] double fs = 0.0, ft = 0.0;
+  auto fold_finish = [&]() __attribute__((always_inline)) {
+    float M;
+    fold_pair_merge(fm, fs, ft, M);
+    if constexpr (NP == 1) {
+      const int x = pw.x0 + 32 * rw + lr;
+      if (hh == 0 && x < W)
+        store_one<float>(args.disp + ((size_t)pw.n * H + pw.y) * W + x, (float)(ft / fs));
+    } else {
+      const double to = ft + (double)pw.dp * fs;
+      if (pw.pass == 0) {
+        f_m = M;
+        f_s = fs;
+        f_t = to;
+      } else {
+        fused_two_pass_store(args, pw, rw, lr, hh, f_m, f_s, f_t, M, fs, to);
+      }
+    }
+  };
+  // one block of that fold (the SPEC flags workgroup-uniform: one branch per block)
+  auto fold_one = [&]<int t>() __attribute__((always_inline)) {
+    const bool sc = p_kk != 0, xl = pw.js < 0;
+    if (!sc && !xl)
+      fold_block<T, MEAN, false, false, FoldF32, t>(acc[t], args, pw, -p_kk, 0, rw, lr, hh, fm, fs, ft);
+    else if (sc && !xl)
+      fold_block<T, MEAN, true, false, FoldF32, t>(acc[t], args, pw, -p_kk, 0, rw, lr, hh, fm, fs, ft);
+    else if (!sc)
+      fold_block<T, MEAN, false, true, FoldF32, t>(acc[t], args, pw, -p_kk, 0, rw, lr, hh, fm, fs, ft);
+    else
+      fold_block<T, MEAN, true, true, FoldF32, t>(acc[t], args, pw, -p_kk, 0, rw, lr, hh, fm, fs, ft);
+  };
   // FUSE: the previous pass's soft-argmin straight from the accumulators (band_common.h), before
   // the next pass's first MFMAs overwrite them; nothing for an invalid segment.  Two D passes
   // without the volume: pass 0's state waits in registers for pass 1.
@@ -483,7 +520,11 @@ __device__ __forceinline__ void sl_role(const Args& args, unsigned char* smem) {
   // previous pass's block t first when SHEAR, and the chunk readouts between them
   // (SPEC: a workgroup-uniform branch around each block's ring writes only; a whole second copy
   // of the step, MFMAs included, made the register allocator spill at the join)
-  auto matrix = [&]<int KS, bool SHEAR>(unsigned lb) __attribute__((always_inline)) {
+  // FOLD (the fused passes' first step, SMCV_SL_FOLD_IL): block t is folded into the previous
+  // pass's soft-argmin right before its MFMAs overwrite it, so the fold's VALU work of block t - 1
+  // issues while block t's MFMAs run (the fold order T-1 .. 0: the same in the volume-kept and the
+  // volume-free pass, which stay bit-identical)
+  auto matrix = [&]<int KS, bool SHEAR, bool FOLD = false>(unsigned lb) __attribute__((always_inline)) {
     const unsigned char* bb = smem + lb + 32 * rw * 32 + swz(lr, hh);
     const f16x8 bh = *reinterpret_cast<const f16x8*>(bb);
     const f16x8 bmv = *reinterpret_cast<const f16x8*>(bb + G::LPL);
@@ -501,6 +542,9 @@ __device__ __forceinline__ void sl_role(const Args& args, unsigned char* smem) {
             const unsigned char* ab = rk + ao;
             const f16x8 ah = *reinterpret_cast<const f16x8*>(ab);
             const f16x8 am = *reinterpret_cast<const f16x8*>(ab + G::RPL);
+            if constexpr (FOLD) {
+              if (p_bytes != 0) fold_one.template operator()<t>();
+            }
             if constexpr (SHEAR && VOL) {
               if constexpr (cr >= 0) drain_read.template operator()<cr>(cv);
               if (__builtin_expect(p_special, 0))
@@ -526,15 +570,29 @@ __device__ __forceinline__ void sl_role(const Args& args, unsigned char* smem) {
     }(std::make_integer_sequence<int, T>{});
   };
   auto first_step = [&]<int KS>(unsigned lb) __attribute__((always_inline)) {
-    fuse_regs();
+    // (not at C = 16 with 7 blocks: its compute wave would spill)
+    constexpr bool FIL = FUSE != 0 && SMCV_SL_FOLD_IL && !(NKS == 1 && T == 7);
+    if constexpr (FIL) {
+      fm = -INFINITY;
+      fs = 0.0;
+      ft = 0.0;
+    } else {
+      fuse_regs();
+    }
     if constexpr (VOL) {
-      matrix.template operator()<KS, true>(lb);
+      matrix.template operator()<KS, true, FIL>(lb);
+      if constexpr (FIL) {
+        if (p_bytes != 0) fold_finish();
+      }
       if constexpr (NKS == 1) {  // the last two chunks now (the next step shears again)
         drain.template operator()<T - 3>();
         drain.template operator()<T - 2>();
       }
     } else {
-      matrix.template operator()<KS, false>(lb);
+      matrix.template operator()<KS, false, FIL>(lb);
+      if constexpr (FIL) {
+        if (p_bytes != 0) fold_finish();
+      }
     }
   };
 
@@ -881,8 +939,10 @@ int band_sl_run(const Args& a0, int64_t N, bool mean, bool aligned4, hipStream_t
       constexpr int FU = decltype(fc)::value;
       if constexpr (FU == 1 && NPC == 2) {
         return (int)SM_EUNSUPPORTED;  // (excluded above)
-      } else if constexpr (FU == 1 && NK == 1 && TM == 7) {
-        if (mean) return fail(SM_EINVAL, "band_sl: unhandled fused mean shape");
+      } else if constexpr (NK == 1 && TM == 7 && NPC == 1) {
+        // the mean at C = 16 with one pass of > 128 disparities is excluded above (its volume-kept
+        // compute wave would spill; its volume-free call pairs with band_h2db's): not compiled
+        if (mean) return fail(SM_EINVAL, "band_sl: unhandled mean shape");
         return launch_sl<false, TM, NK, NPC, NS, FU>(a, N, st);
       } else {
         return mean ? launch_sl<true, TM, NK, NPC, NS, FU>(a, N, st)

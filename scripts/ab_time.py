@@ -97,6 +97,17 @@ def ops():
             1, 134784000),
         "cfg5": (lambda: (lambda L, R: lambda: F.concat_volume(L, R, 64))(*feats((1, 128, 540, 960), torch.float16)),
                  1, 17252352000),
+        # round 6: the stale figures
+        "cfg2_argext": (lambda: (lambda v: lambda: F.hard_argmax(v))(torch.randn(8, 192, 540, 960, device="cuda")),
+                        8, 192 * 540 * 960 * 4 + 540 * 960 * 8),
+        "cfg2_f32": (lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="f32"))(*feats((8, 64, 540, 960), torch.float32)),
+                     8, 663552000),
+        "cfg2_valu": (lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192, algo="valu"))(*feats((2, 64, 540, 960), torch.float32)),
+                      2, 663552000),
+        "cfg2_b32_auto": (lambda: (lambda L, R: lambda: F.inner_product_volume(L, R, 192))(*feats((32, 64, 540, 960), torch.float32)),
+                          32, 663552000),
+        **{f"ragged_{w}": (lambda w=w: (lambda L, R: lambda: F.inner_product_volume(L, R, 192))(*feats((8, 64, 540, w), torch.float32)),
+                           8, (2 * 64 + 192) * 540 * w * 4) for w in (928, 944, 952, 956, 957, 958, 959, 960)},
     }
 
 
