@@ -306,6 +306,7 @@ __device__ __forceinline__ void sl_role(const Args& args, unsigned char* smem) {
   bool p_full = false;     // the whole 128-pixel segment and all DMAX disparities are stored
   float* p_ob = static_cast<float*>(args.out);
   const int64_t plane_stride = (int64_t)H * W;
+  const bool nt_rows = __builtin_amdgcn_readfirstlane(W % 16 == 0 ? 1 : 0) != 0;
   // volume-free fused pass with two D passes: pass 0's soft-argmin state of the lane pair's pixel
   [[maybe_unused]] float f_m = 0.f;
   [[maybe_unused]] double f_s = 0.0, f_t = 0.0;
@@ -383,21 +384,28 @@ __device__ __forceinline__ void sl_role(const Args& args, unsigned char* smem) {
         __builtin_amdgcn_make_buffer_rsrc(cb, (short)0, p_bytes, 0x00020000);
     const unsigned q8 = (unsigned)(8 * plane_stride * 4);
     const unsigned lo = (unsigned)(rr * plane_stride * 4 + 16 * cc);
+    // non-temporal stores when the volume rows are 64-B aligned (W % 16 == 0: every 128-B
+    // piece of a store fills whole 64-B halves of lines); otherwise a piece straddles two lines
+    // that a neighbouring wave completes, and plain stores let L2 merge the halves before the
+    // write-back (W = 952 / 956: 1,517 / 1,557 against 1,903 / 2,209 us per 8-pair launch,
+    // profiles/r06/stale/r6r_*; W = 928 / 944 / 960 as fast or faster non-temporal)
+    auto st = [&](const f32x4v& v, unsigned off) __attribute__((always_inline)) {
+      const auto u = __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v);
+      if (SMCV_SL_NTSTORE && nt_rows)
+        __builtin_amdgcn_raw_buffer_store_b128(u, rsrc, off, 0, 2);
+      else
+        __builtin_amdgcn_raw_buffer_store_b128(u, rsrc, off, 0, 0);
+    };
     if (p_full) {  // every cell of the chunk is inside the volume
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq)
-        __builtin_amdgcn_raw_buffer_store_b128(
-            __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, vp[qq]), rsrc,
-            lo + (unsigned)qq * q8, 0, SMCV_SL_NTSTORE ? 2 : 0);
+      for (int qq = 0; qq < 4; ++qq) st(vp[qq], lo + (unsigned)qq * q8);
     } else {
       // masked lanes: the offset's top bit set (out of range, dropped)
       const unsigned xbad = (unsigned)(pw.x0 + 32 * rw + 4 * cc >= W) << 31;
 #pragma unroll
       for (int qq = 0; qq < 4; ++qq) {
         const unsigned bad = xbad | ((unsigned)(32 * c + 8 * qq + rr >= pw.Dp) << 31);
-        __builtin_amdgcn_raw_buffer_store_b128(
-            __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, vp[qq]), rsrc,
-            (lo + (unsigned)qq * q8) | bad, 0, SMCV_SL_NTSTORE ? 2 : 0);
+        st(vp[qq], (lo + (unsigned)qq * q8) | bad);
       }
     }
   };
