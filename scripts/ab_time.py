@@ -97,6 +97,11 @@ def ops():
             1, 134784000),
         "cfg5": (lambda: (lambda L, R: lambda: F.concat_volume(L, R, 64))(*feats((1, 128, 540, 960), torch.float16)),
                  1, 17252352000),
+        # round 6: cfg5's output written by torch's sequential fill, the store-pattern ceiling
+        "cfg5_fill": (lambda: (lambda o: lambda: o.zero_())(torch.empty(1, 256, 540, 960, 64, dtype=torch.float16, device="cuda")),
+                      1, 17252352000),
+        "cfg5_iw": (lambda: (lambda L, R: lambda: F.interweave_volume(L, R, 64))(*feats((1, 128, 540, 960), torch.float16)),
+                    1, 17252352000),
         # round 6: the stale figures
         "cfg2_argext": (lambda: (lambda v: lambda: F.hard_argmax(v))(torch.randn(8, 192, 540, 960, device="cuda")),
                         8, 192 * 540 * 960 * 4 + 540 * 960 * 8),
