@@ -7,7 +7,7 @@ Workloads (--config, BASELINE.json configs[1..4]; inputs synthetic and already r
                   (model/mobile_disp_net_c.py:208-220).  Global batch 32, split 32/k over k GPUs
                   (strong scaling).
   cfg3            1x256x540x960 bf16, groupwise volume G=8 D=192, fp32 (N,G,H,W,D) out
-                  (TorchGroupwiseCost, cost_volume/groupwise.py:24-56).  One pair per GPU.
+                  (TorchGroupwiseCost, cost_volume/groupwise.py:24-56).  4 pairs per GPU, one launch.
   cfg4            16x1080x1920 fp32 per pair, correlation volume D=256 (mean over C,
                   model/mobile_disp_net_c.py:188-205) + soft-argmin; global batch 32 split 32/k
                   (strong scaling, configs[3] / mobile_disp_net_c.py:365-367).
@@ -60,8 +60,10 @@ CONFIGS = {
                  global_batch=32, chunk=32, dname="f32",
                  workload="BASELINE configs[1]: mobile_stereo_net inner_product CV, 1/4-res KITTI "
                           "540x960, C=64, D=192, fp32 + soft-argmin regression"),
+    # cfg3: 4 pairs per GPU in one launch (round 6; one pair per launch leaves the persistent grid's
+    # ramp and tail in every 0.73 ms launch: 0.62-0.64 against 0.71 at 4 pairs, profiles/r06/ab/r6v_*)
     "cfg3": dict(C=256, H=540, W=960, D=192, G=8, dtype=torch.bfloat16, op="groupwise",
-                 regress=False, global_batch=None, chunk=1, dname="bf16",
+                 regress=False, global_batch=None, per_gpu=4, chunk=4, dname="bf16",
                  workload="BASELINE configs[2]: groupwise cost volume, G=8 C=256 D=192 at 540x960, "
                           "bf16 in, fp32 (N,G,H,W,D) out, MFMA path"),
     "cfg4": dict(C=16, H=1080, W=1920, D=256, dtype=torch.float32, op="correlation", regress=True,
@@ -498,8 +500,9 @@ def main():
         nb = a.batch
     else:
         gb = a.global_batch or cfg["global_batch"]
-        if gb is None:  # one-GPU configs: one pair per GPU (replicas)
-            scaling, global_batch, nb = "weak", world, 1
+        if gb is None:  # one-GPU configs: a fixed number of pairs per GPU (replicas)
+            nb = cfg.get("per_gpu", 1)
+            scaling, global_batch = "weak", world * nb
         else:
             scaling, global_batch = "strong", gb
             s, e = shard_range(gb, rank, world)
