@@ -290,6 +290,10 @@ __device__ __forceinline__ int exp_of(float x) { return __builtin_amdgcn_frexp_e
 #ifndef SMCV_FOLD_FMA
 #define SMCV_FOLD_FMA 1  // band_sl's fused fold: 1/C and 2^kk folded into the exponent's FMA (0:
 #endif                   // the cells scaled one by one; cfg4 volume-free 5 % slower, r05)
+#ifndef SMCV_FOLD_PK
+#define SMCV_FOLD_PK 1  // FoldFma's (band_sl's) per-cell exponent, sum and weighted sum as packed
+#endif                  // fp32 pairs (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32): cfg4 volume-free
+                        // -9 %, cfg2 -4 %, volume kept flat (profiles/r06/ab/r6w_*, round 6)
 #ifndef SMCV_SCHED_IL
 #define SMCV_SCHED_IL 0  // diagnostic: chunks of IL segments dealt round-robin to the XCD groups
 #endif                   // instead of one contiguous range each (IL a multiple of 8)
@@ -416,7 +420,8 @@ __device__ __forceinline__ void slow_softargmin_f32(const Args& args, const Work
 // RT = FoldFma: the fp32 cells with 1/C and 2^kk folded into the exponent's FMA (the cells stay
 // raw; their block maximum is scaled once, K > 0 keeps it the maximum): e = 2^(fma(x, K, -sh)
 // log2 e), two operations per cell instead of the scale, subtract and multiply.  A kernel pair
-// whose volume-kept and volume-free calls must agree bit for bit uses the same RT.
+// whose volume-kept and volume-free calls must agree bit for bit uses the same RT.  SMCV_FOLD_PK:
+// FoldFma folds the cells in packed fp32 pairs (even / odd partial sums).
 struct FoldFma {};
 using FoldF32 = std::conditional<SMCV_FOLD_FMA != 0, FoldFma, float>::type;
 
@@ -458,6 +463,23 @@ __device__ __forceinline__ void fold_block(const f32x16& blk, const Args& args, 
       // needed a clamp at 2e38)  No clamp: x K - sh <= 0, and a result below
       // -FLT_MAX rounds to -inf, e = 0.
       const float nsh = -sh;
+#if SMCV_FOLD_PK
+      // cells (2j, 2j+1) as one packed pair: the same per-cell arithmetic, two partial sums per
+      // lane (even and odd cells) added at the end
+      typedef float f32x2 __attribute__((ext_vector_type(2)));
+      const f32x2 K2 = {K, K}, N2 = {nsh, nsh}, L2 = {kL2E, kL2E};
+      f32x2 ps2 = {0.f, 0.f}, pc2 = {0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < 16; i += 2) {
+        const f32x2 x2 = {v[i], v[i + 1]};
+        const f32x2 y2 = __builtin_elementwise_fma(x2, K2, N2) * L2;
+        const f32x2 e2 = {__builtin_amdgcn_exp2f(y2.x), __builtin_amdgcn_exp2f(y2.y)};
+        const f32x2 c2 = {(float)((i & 3) + 8 * (i >> 2)), (float)(((i + 1) & 3) + 8 * (i >> 2))};
+        ps2 += e2;
+        pc2 = __builtin_elementwise_fma(c2, e2, pc2);
+      }
+      const float ps = ps2.x + ps2.y, pc = pc2.x + pc2.y;
+#else
       float ps = 0.f, pc = 0.f;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
@@ -465,6 +487,7 @@ __device__ __forceinline__ void fold_block(const f32x16& blk, const Args& args, 
         ps += e;
         pc = fmaf((float)((i & 3) + 8 * (i >> 2)), e, pc);
       }
+#endif
       s = s * (double)f + (double)ps;
       tt = tt * (double)f + (double)ub * (double)ps - (double)pc;
       m = nm;
@@ -485,6 +508,8 @@ __device__ __forceinline__ void fold_block(const f32x16& blk, const Args& args, 
     const float nm = fmaxf(m, bm);
     const float sh = fmaxf(nm, -3.402823466e38f);
     const float f = __builtin_amdgcn_exp2f((m - sh) * kL2E);
+    // (scalar also under SMCV_FOLD_PK: packed, band_h2's fp16 volume-free pass measured 0.7 %
+    // slower, profiles/r06/ab/r6w_*, and band_rs / band_h2db FUSE 1 spill with the pairs)
     float ps = 0.f, pc = 0.f;  // sum e, sum c_i e
 #pragma unroll
     for (int i = 0; i < 16; ++i) {

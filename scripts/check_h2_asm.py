@@ -174,7 +174,7 @@ def main():
             asm = open(out).read()
             bad += check(asm)
             n += len(kernels(asm))
-    for b in bad[:40]:
+    for b in bad[:int(os.environ.get("SHOW", 40))]:
         print(b)
     print(f"{n} kernels checked, {len(bad)} problems")
     if n == 0:
