@@ -305,6 +305,8 @@ __global__ __launch_bounds__(kThreads, wg_per_cu<FUSE>()) void band_h2(Args args
           c = mma(ah[t % NB], bm, c);
         }
         acc[t] = mma(ah[t % NB], bh, c);
+      } else {  // diagnostic: operands consumed, accumulators opaque (the epilogue stays whole)
+        asm volatile("" : "+v"(acc[t]) : "v"(ah[t % NB]), "v"(bh));
       }
       __builtin_amdgcn_sched_barrier(0);
     }

@@ -560,8 +560,8 @@ __device__ __forceinline__ void sl_role(const Args& args, unsigned char* smem) {
               else
                 write_block.template operator()<t, false>();
             }
-            if constexpr (SMCV_SL_ABLATE & 8) {
-              asm volatile("" : : "v"(ah), "v"(am), "v"(bh), "v"(bmv));
+            if constexpr (SMCV_SL_ABLATE & 8) {  // accumulators opaque: the fold stays whole
+              asm volatile("" : "+v"(acc[t]) : "v"(ah), "v"(am), "v"(bh), "v"(bmv));
             } else {
               f32x16 c;
               if constexpr (KS == 0)
