@@ -460,8 +460,11 @@ __device__ __forceinline__ void fold_block(const f32x16& blk, const Args& args, 
       // then scaled: the exponent's error is relative to x K - sh, not to |x K|.  (Round 5's
       // one-FMA form x (K log2 e) - sh log2 e carried an error of 2^-24 |sh| log2 e: fine for
       // cells of O(10), but cells of 1e30 lost the maximum's own weight, NaN, and the shift
-      // needed a clamp at 2e38)  No clamp: x K - sh <= 0, and a result below
-      // -FLT_MAX rounds to -inf, e = 0.
+      // needed a clamp at 2e38)  No clamp: x K - sh <= 0 when K is a power of two
+      // (the sum, the mean over 2^k channels, the 2^kk scales: bm K exact), and a result below
+      // -FLT_MAX rounds to -inf, e = 0.  For other K, sh = bm K rounded can sit half an ulp below
+      // the maximum cell's product, whose exponent is then that residual (<= 2^-25 |sh|): it
+      // overflows exp2 only for |sh| > 2^32.
       const float nsh = -sh;
 #if SMCV_FOLD_PK
       // cells (2j, 2j+1) as one packed pair: the same per-cell arithmetic, two partial sums per
